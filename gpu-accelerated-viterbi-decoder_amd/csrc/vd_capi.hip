@@ -1,0 +1,324 @@
+// vd_capi.hip -- C-ABI runtime of the MI355X Viterbi decoder (see include/vd_capi.h).
+//
+// Replaces the reference's ViterbiCUDA<options> implementation (src/viterbi/viterbi.cu:10-139,210-262):
+// decoder objects own reusable device buffers and a stream; vd_run is the blocking host-to-host
+// call with kernel-only event timing like the reference; vd_run_device is the allocation-free,
+// sync-free device path; vd_run_batches shards independent batches over the devices of a node.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+#include <chrono>
+
+#include "../../include/vd_capi.h"
+#include "vd_kernels.h"
+#include "vd_synth.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg)
+{
+    g_err = msg;
+    return code;
+}
+
+#define VD_HIP(expr)                                                                         \
+    do {                                                                                     \
+        hipError_t e_ = (expr);                                                              \
+        if (e_ != hipSuccess)                                                                \
+            return fail(e_ == hipErrorOutOfMemory ? VD_ERR_NOMEM : VD_ERR_DEVICE,            \
+                        std::string(#expr) + ": " + hipGetErrorString(e_));                  \
+    } while (0)
+
+int ch_of(int o) { return o & 0xF; }
+int met_of(int o) { return (o >> 4) & 0xF; }
+int out_of(int o) { return (o >> 8) & 0xF; }
+int comp_of(int o) { return (o >> 12) & 0xF; }
+int bpp_of(int o) { return out_of(o) == 1 ? 16 : 32; }
+
+bool valid(int o)
+{
+    if (o & ~0xFFFF) return false;
+    int ch = ch_of(o), me = met_of(o), out = out_of(o), cm = comp_of(o);
+    if (ch > 4 || me > 2 || out > 1 || cm > 1) return false;
+    // OptionsValid (viterbi.h:22-41)
+    if (ch == 2 && me == 2) return false;
+    if (ch == 3 && me == 2) return false;
+    if (ch == 3 && me == 1) return false;
+    if (me == 2 && cm == 1) return false;
+    return true;
+}
+
+size_t input_size(int o, size_t n)
+{
+    switch (ch_of(o)) {
+    case 0: return (n + 7) / 8;
+    case 1: return (n + 1) / 2;
+    case 2: return n;
+    case 3: return n * 2;
+    case 4: return n * 4;
+    }
+    return 0;
+}
+size_t message_len(int o, size_t n)
+{
+    if (n / 2 < 64) return 0;  // the reference underflows here (size_t); rejected instead
+    size_t bpp = (size_t)bpp_of(o);
+    return (n / 2 - 64) / bpp * bpp;
+}
+// stages whose channel data lies in whole 32-bit words of the caller's buffer
+uint64_t avail_stages(int o, size_t n)
+{
+    size_t words = input_size(o, n) / 4;
+    uint64_t per = 0;
+    switch (ch_of(o)) {
+    case 0: per = words * 16; break;
+    case 1: per = words * 4; break;
+    case 2: per = words * 2; break;
+    case 3: per = words; break;
+    case 4: per = words / 2; break;
+    }
+    uint64_t half = n / 2;
+    return per < half ? per : half;
+}
+
+using launch_fn = void (*)(const void*, void*, vd::Geom, hipStream_t);
+
+template <int CH, int CORE, int OB>
+void launch_t(const void* in, void* out, vd::Geom g, hipStream_t s)
+{
+    if constexpr (CORE == vd::B32)
+        hipLaunchKernelGGL((vd::vd_decode_b32<CH, OB>), dim3(g.nchunks), dim3(64), 0, s, in, out, g);
+    else
+        hipLaunchKernelGGL((vd::vd_decode_pk<CH, CORE, OB>), dim3((g.nchunks + 1) / 2), dim3(64), 0, s, in, out, g);
+}
+
+template <int CH, int CORE>
+launch_fn pick_ob(int ob)
+{
+    return ob == 1 ? &launch_t<CH, CORE, 16> : &launch_t<CH, CORE, 32>;
+}
+
+launch_fn pick(int o)
+{
+    const int ch = ch_of(o), me = met_of(o), ob = out_of(o);
+    switch (ch) {
+    case 0: return me == 0 ? pick_ob<0, 0>(ob) : me == 1 ? pick_ob<0, 1>(ob) : pick_ob<0, 2>(ob);
+    case 1: return me == 0 ? pick_ob<1, 0>(ob) : me == 1 ? pick_ob<1, 1>(ob) : pick_ob<1, 2>(ob);
+    case 2: return me == 0 ? pick_ob<2, 0>(ob) : pick_ob<2, 1>(ob);
+    case 3: return pick_ob<3, 0>(ob);
+    case 4: return me == 0 ? pick_ob<4, 0>(ob) : me == 1 ? pick_ob<4, 1>(ob) : pick_ob<4, 2>(ob);
+    }
+    return nullptr;
+}
+
+const char* kname(int o)
+{
+    static const char* names[5][3] = {
+        {"vd_decode_b32<HARD>", "vd_decode_pk<HARD,B16>", "vd_decode_pk<HARD,F16>"},
+        {"vd_decode_b32<SOFT4>", "vd_decode_pk<SOFT4,B16>", "vd_decode_pk<SOFT4,F16>"},
+        {"vd_decode_b32<SOFT8>", "vd_decode_pk<SOFT8,B16>", "-"},
+        {"vd_decode_b32<SOFT16>", "-", "-"},
+        {"vd_decode_b32<FP32>", "vd_decode_pk<FP32,B16>", "vd_decode_pk<FP32,F16>"},
+    };
+    if (!valid(o)) return "-";
+    return names[ch_of(o)][met_of(o)];
+}
+
+}  // namespace
+
+struct vd_decoder {
+    int options = 0;
+    int device = 0;
+    void* in_d = nullptr;
+    void* out_d = nullptr;
+    size_t cap_in = 0, cap_out = 0;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+};
+
+static int ensure_capacity(vd_decoder* d, size_t inBytes, size_t outBytes)
+{
+    if (inBytes > d->cap_in) {
+        if (d->in_d) (void)hipFree(d->in_d);
+        d->in_d = nullptr;
+        d->cap_in = 0;
+        VD_HIP(hipMalloc(&d->in_d, inBytes));
+        d->cap_in = inBytes;
+    }
+    if (outBytes > d->cap_out) {
+        if (d->out_d) (void)hipFree(d->out_d);
+        d->out_d = nullptr;
+        d->cap_out = 0;
+        VD_HIP(hipMalloc(&d->out_d, outBytes));
+        d->cap_out = outBytes;
+    }
+    return VD_OK;
+}
+
+static int launch_decode(int options, const void* in_d, void* out_d, size_t inputNum, hipStream_t s)
+{
+    launch_fn f = pick(options);
+    if (!f) return fail(VD_ERR_OPTIONS, "invalid options");
+    size_t msg = message_len(options, inputNum);
+    vd::Geom g;
+    g.packNum = msg / (size_t)bpp_of(options);
+    g.availStages = avail_stages(options, inputNum);
+    g.nchunks = vd::kChunks;
+    if (g.packNum == 0) return VD_OK;
+    f(in_d, out_d, g, s);
+    VD_HIP(hipGetLastError());
+    return VD_OK;
+}
+
+extern "C" {
+
+int vd_options_valid(int options) { return valid(options) ? 1 : 0; }
+size_t vd_input_size(int options, size_t n) { return input_size(options, n); }
+size_t vd_message_len(int options, size_t n) { return message_len(options, n); }
+size_t vd_output_size(int options, size_t n) { return message_len(options, n) / 8; }
+int vd_num_chunks(void) { return vd::kChunks; }
+const char* vd_last_error(void) { return g_err.c_str(); }
+const char* vd_kernel_name(int options) { return kname(options); }
+
+int vd_device_count(void)
+{
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+int vd_create(int options, size_t preallocInputNum, int device, vd_decoder** out)
+{
+    if (!out) return fail(VD_ERR_ARG, "null output handle");
+    *out = nullptr;
+    if (!valid(options)) return fail(VD_ERR_OPTIONS, "options disabled by OptionsValid");
+    int ndev = 0;
+    VD_HIP(hipGetDeviceCount(&ndev));
+    if (device < 0 || device >= ndev) return fail(VD_ERR_ARG, "device index out of range");
+    VD_HIP(hipSetDevice(device));
+    vd_decoder* d = new vd_decoder();
+    d->options = options;
+    d->device = device;
+    if (hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreate(&d->ev0) != hipSuccess || hipEventCreate(&d->ev1) != hipSuccess) {
+        vd_destroy(d);
+        return fail(VD_ERR_DEVICE, "stream/event creation failed");
+    }
+    if (preallocInputNum) {
+        int rc = ensure_capacity(d, input_size(options, preallocInputNum),
+                                 message_len(options, preallocInputNum) / 8 + 16);
+        if (rc != VD_OK) { vd_destroy(d); return rc; }
+    }
+    *out = d;
+    return VD_OK;
+}
+
+int vd_destroy(vd_decoder* d)
+{
+    if (!d) return VD_OK;
+    (void)hipSetDevice(d->device);
+    if (d->in_d) (void)hipFree(d->in_d);
+    if (d->out_d) (void)hipFree(d->out_d);
+    if (d->ev0) (void)hipEventDestroy(d->ev0);
+    if (d->ev1) (void)hipEventDestroy(d->ev1);
+    if (d->stream) (void)hipStreamDestroy(d->stream);
+    delete d;
+    return VD_OK;
+}
+
+int vd_run(vd_decoder* d, const void* input_h, void* output_h, size_t inputNum, float* kernel_ms)
+{
+    if (!d || !input_h || !output_h) return fail(VD_ERR_ARG, "null argument");
+    const size_t inB = input_size(d->options, inputNum), outB = message_len(d->options, inputNum) / 8;
+    if (message_len(d->options, inputNum) == 0) return fail(VD_ERR_ARG, "inputNum too small");
+    VD_HIP(hipSetDevice(d->device));
+    int rc = ensure_capacity(d, inB, outB + 16);
+    if (rc != VD_OK) return rc;
+    VD_HIP(hipMemcpyAsync(d->in_d, input_h, inB, hipMemcpyHostToDevice, d->stream));
+    VD_HIP(hipEventRecord(d->ev0, d->stream));
+    rc = launch_decode(d->options, d->in_d, d->out_d, inputNum, d->stream);
+    if (rc != VD_OK) return rc;
+    VD_HIP(hipEventRecord(d->ev1, d->stream));
+    VD_HIP(hipMemcpyAsync(output_h, d->out_d, outB, hipMemcpyDeviceToHost, d->stream));
+    VD_HIP(hipStreamSynchronize(d->stream));
+    if (kernel_ms) VD_HIP(hipEventElapsedTime(kernel_ms, d->ev0, d->ev1));
+    return VD_OK;
+}
+
+int vd_run_device(vd_decoder* d, const void* input_d, void* output_d, size_t inputNum, void* stream)
+{
+    if (!d || !input_d || !output_d) return fail(VD_ERR_ARG, "null argument");
+    if (message_len(d->options, inputNum) == 0) return fail(VD_ERR_ARG, "inputNum too small");
+    return launch_decode(d->options, input_d, output_d, inputNum, (hipStream_t)stream);
+}
+
+int vd_run_batches(int options, const void* const* input_h, void* const* output_h, size_t inputNum,
+                   int nbatches, const int* devices, int ndev, float* wall_ms)
+{
+    if (!valid(options)) return fail(VD_ERR_OPTIONS, "options disabled by OptionsValid");
+    if (!input_h || !output_h || !devices || ndev <= 0 || nbatches < 0) return fail(VD_ERR_ARG, "bad arguments");
+    std::vector<vd_decoder*> decs(ndev, nullptr);
+    for (int i = 0; i < ndev; i++) {
+        int rc = vd_create(options, inputNum, devices[i], &decs[i]);
+        if (rc != VD_OK) {
+            for (auto* x : decs) vd_destroy(x);
+            return rc;
+        }
+    }
+    std::vector<int> rcs(ndev, VD_OK);
+    std::vector<std::string> errs(ndev);
+    auto t0 = std::chrono::steady_clock::now();
+    std::vector<std::thread> th;
+    for (int i = 0; i < ndev; i++) {
+        th.emplace_back([&, i]() {
+            for (int b = i; b < nbatches; b += ndev) {
+                int rc = vd_run(decs[i], input_h[b], output_h[b], inputNum, nullptr);
+                if (rc != VD_OK) { rcs[i] = rc; errs[i] = g_err; return; }
+            }
+        });
+    }
+    for (auto& t : th) t.join();
+    auto t1 = std::chrono::steady_clock::now();
+    for (auto* x : decs) vd_destroy(x);
+    for (int i = 0; i < ndev; i++)
+        if (rcs[i] != VD_OK) return fail(rcs[i], errs[i]);
+    if (wall_ms) *wall_ms = std::chrono::duration<float, std::milli>(t1 - t0).count();
+    return VD_OK;
+}
+
+int vd_synth_device(int options, size_t N, float snr, uint64_t seed, void* bits_d, void* packed_d, void* stream)
+{
+    if (!valid(options)) return fail(VD_ERR_OPTIONS, "options disabled by OptionsValid");
+    if (N % 16 || !packed_d) return fail(VD_ERR_ARG, "N must be a multiple of 16");
+    hipStream_t s = (hipStream_t)stream;
+    const float sigma = (float)std::pow(10.0, -(double)snr / 5.0);
+    const int noiseless = std::isinf(snr) && snr > 0 ? 1 : 0;
+    const uint64_t nval = 2 * (uint64_t)N;
+    const int per = ch_of(options) == 0 ? 32 : ch_of(options) == 1 ? 8 : ch_of(options) == 2 ? 4 : ch_of(options) == 3 ? 2 : 1;
+    const uint64_t nwords = nval / per;
+    const dim3 blk(256), grd((unsigned)((nwords + 255) / 256));
+    switch (ch_of(options)) {
+    case 0: hipLaunchKernelGGL(vd::synth_pack<0>, grd, blk, 0, s, seed, nval, sigma, noiseless, packed_d); break;
+    case 1: hipLaunchKernelGGL(vd::synth_pack<1>, grd, blk, 0, s, seed, nval, sigma, noiseless, packed_d); break;
+    case 2: hipLaunchKernelGGL(vd::synth_pack<2>, grd, blk, 0, s, seed, nval, sigma, noiseless, packed_d); break;
+    case 3: hipLaunchKernelGGL(vd::synth_pack<3>, grd, blk, 0, s, seed, nval, sigma, noiseless, packed_d); break;
+    case 4: hipLaunchKernelGGL(vd::synth_pack<4>, grd, blk, 0, s, seed, nval, sigma, noiseless, packed_d); break;
+    }
+    VD_HIP(hipGetLastError());
+    if (bits_d) {
+        hipLaunchKernelGGL(vd::synth_bits, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, s, seed, (uint64_t)N,
+                           (uint8_t*)bits_d);
+        VD_HIP(hipGetLastError());
+    }
+    return VD_OK;
+}
+
+}  // extern "C"

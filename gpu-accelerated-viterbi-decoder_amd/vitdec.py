@@ -1,0 +1,219 @@
+"""vitdec -- Python binding of the MI355X Viterbi decoder's C-ABI (include/vd_capi.h).
+
+Mirrors the reference's decoder interface `ViterbiCUDA<options>` (src/viterbi/viterbi.h:43-152):
+the same option bitmask, the same constexpr members (constLen, polyn1, polyn2, extraL, extraR,
+bitsPerPack, encDataPerPack, ...), the same size helpers and the same `run(input, output, inputNum)`
+call returning the kernel time in ms.  Errors raise VitdecError (the reference exits the process,
+gpuerrors.h:8-17; the C++ header include/viterbi.h keeps that behaviour).
+
+Device-side entry points (`run_device`, `synth_device`) take raw device pointers, e.g.
+`tensor.data_ptr()` of a torch tensor on the decoder's device, and a HIP stream handle
+(`torch.cuda.current_stream().cuda_stream`).  torch is only plumbing for memory and streams.
+
+There is no CPU fallback: if lib/libvitdec.so is missing or no GPU is visible, decoding raises.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libvitdec.so")
+
+# ---- option bitmask (reference src/viterbi/viterbi.h:7-20) ----
+CHANNEL_MASK, METRIC_MASK, DECODE_MASK, COMP_MASK = 0xF, 0xF0, 0xF00, 0xF000
+HARD, SOFT4, SOFT8, SOFT16, FP32 = 0x0, 0x1, 0x2, 0x3, 0x4
+M_B32, M_B16, M_FP16 = 0x00, 0x10, 0x20
+O_B32, O_B16 = 0x000, 0x100
+REG, DPX = 0x0000, 0x1000
+
+INPUT_NAMES = {"HARD": HARD, "h": HARD, "SOFT4": SOFT4, "s4": SOFT4, "SOFT8": SOFT8, "s8": SOFT8,
+               "SOFT16": SOFT16, "s16": SOFT16, "FP32": FP32, "f": FP32}
+METRIC_NAMES = {"b16": M_B16, "b32": M_B32, "f16": M_FP16}
+OUTPUT_NAMES = {"b16": O_B16, "b32": O_B32}
+COMP_NAMES = {"REG": REG, "reg": REG, "DPX": DPX, "dpx": DPX}
+
+VD_OK = 0
+_ERRNAMES = {-1: "VD_ERR_OPTIONS", -2: "VD_ERR_ARG", -3: "VD_ERR_DEVICE", -4: "VD_ERR_NOMEM",
+             -5: "VD_ERR_NOKERNEL"}
+
+# every entry point declared in include/vd_capi.h (tests check the library exports all of them)
+EXPORTS = ["vd_options_valid", "vd_input_size", "vd_message_len", "vd_output_size", "vd_num_chunks",
+           "vd_create", "vd_destroy", "vd_run", "vd_run_device", "vd_run_batches", "vd_synth_device",
+           "vd_simulate_host", "vd_count_errors", "vd_last_error", "vd_device_count", "vd_kernel_name"]
+
+
+class VitdecError(RuntimeError):
+    pass
+
+
+_lib = None
+
+
+def lib():
+    """Load lib/libvitdec.so (raises if the HIP extension has not been built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise VitdecError(f"{LIB_PATH} not built: run `make -C {_HERE}` (or __graft_entry__.build())")
+    L = ctypes.CDLL(LIB_PATH)
+    sz, vp, i, f = ctypes.c_size_t, ctypes.c_void_p, ctypes.c_int, ctypes.c_float
+    L.vd_options_valid.argtypes = [i]
+    for n in ("vd_input_size", "vd_message_len", "vd_output_size"):
+        getattr(L, n).argtypes = [i, sz]
+        getattr(L, n).restype = sz
+    L.vd_create.argtypes = [i, sz, i, ctypes.POINTER(vp)]
+    L.vd_destroy.argtypes = [vp]
+    L.vd_run.argtypes = [vp, vp, vp, sz, ctypes.POINTER(f)]
+    L.vd_run_device.argtypes = [vp, vp, vp, sz, vp]
+    L.vd_run_batches.argtypes = [i, ctypes.POINTER(vp), ctypes.POINTER(vp), sz, i, ctypes.POINTER(i), i,
+                                 ctypes.POINTER(f)]
+    L.vd_synth_device.argtypes = [i, sz, f, ctypes.c_uint64, vp, vp, vp]
+    L.vd_simulate_host.argtypes = [i, sz, f, ctypes.c_uint32, ctypes.c_uint32, vp, vp]
+    L.vd_count_errors.argtypes = [i, vp, sz, vp, sz]
+    L.vd_count_errors.restype = ctypes.c_longlong
+    L.vd_last_error.restype = ctypes.c_char_p
+    L.vd_kernel_name.argtypes = [i]
+    L.vd_kernel_name.restype = ctypes.c_char_p
+    _lib = L
+    return L
+
+
+def _check(rc):
+    if rc != VD_OK:
+        msg = lib().vd_last_error().decode(errors="replace")
+        raise VitdecError(f"{_ERRNAMES.get(rc, rc)}: {msg}")
+
+
+def parse_options(input="HARD", metric="b32", output="b32", comp="REG"):
+    """CLI-style names (reference src/main.cpp:174-264) -> options bitmask."""
+    return INPUT_NAMES[input] | METRIC_NAMES[metric] | OUTPUT_NAMES[output] | COMP_NAMES[comp]
+
+
+def options_valid(options):
+    return bool(lib().vd_options_valid(options))
+
+
+def device_count():
+    return lib().vd_device_count()
+
+
+def kernel_name(options):
+    return lib().vd_kernel_name(options).decode()
+
+
+class ViterbiCUDA:
+    """The reference's ViterbiCUDA<options> (viterbi.h:43-152) over the C-ABI."""
+
+    constLen = 7
+    polyn1 = 0o171
+    polyn2 = 0o133
+    extraL_raw = extraR_raw = slideSize_raw = 32
+    bmMemWidth = 32
+    blockDimY = 2
+    FPprecision = 4
+
+    def __init__(self, options, inputNum=0, device=0):
+        if not options_valid(options):
+            raise VitdecError(f"options 0x{options:x} disabled by OptionsValid")
+        self.options = options
+        self.inputType = options & CHANNEL_MASK
+        self.metricType = options & METRIC_MASK
+        self.outputType = options & DECODE_MASK
+        self.compMode = options & COMP_MASK
+        self.bitsPerMetric = {M_B16: 16, M_B32: 32}.get(self.metricType, 11)
+        self.bitsPerPack = 16 if self.outputType == O_B16 else 32
+        rnd = lambda a, b: (a + b - 1) // b * b
+        self.extraL = rnd(32, self.bitsPerPack) - (self.constLen - 1)
+        self.extraR = rnd(32, self.bitsPerPack) + (self.constLen - 1)
+        self.slideSize = rnd(32, self.bitsPerPack)
+        self.forwardLen = self.extraL + self.slideSize + self.extraR
+        self.encDataPerPack = {HARD: 32, SOFT4: 8, SOFT8: 4, SOFT16: 2, FP32: 1}[self.inputType]
+        self.encDataWidth = {HARD: 1, SOFT4: 4, SOFT8: 8, SOFT16: 16, FP32: self.FPprecision}[self.inputType]
+        self.encPack_t = np.float32 if self.inputType == FP32 else np.int32
+        self.decPack_t = np.uint16 if self.outputType == O_B16 else np.uint32
+        self.device = device
+        h = ctypes.c_void_p()
+        _check(lib().vd_create(options, inputNum, device, ctypes.byref(h)))
+        self._h = h
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().vd_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    # size helpers (viterbi.cu:63-92)
+    def getInputSize(self, inputNum):
+        return lib().vd_input_size(self.options, inputNum)
+
+    def getMessageLen(self, inputNum):
+        return lib().vd_message_len(self.options, inputNum)
+
+    def getOutputSize(self, inputNum):
+        return lib().vd_output_size(self.options, inputNum)
+
+    def run(self, input_h, output_h=None, inputNum=None):
+        """Blocking host decode (viterbi.cu:210-238). Returns (output array, kernel ms)."""
+        input_h = np.ascontiguousarray(input_h)
+        if inputNum is None:
+            inputNum = input_h.size * self.encDataPerPack
+        if input_h.nbytes < self.getInputSize(inputNum):
+            raise VitdecError("input buffer smaller than getInputSize(inputNum)")
+        if output_h is None:
+            output_h = np.zeros(self.getOutputSize(inputNum) // np.dtype(self.decPack_t).itemsize,
+                                dtype=self.decPack_t)
+        if output_h.nbytes < self.getOutputSize(inputNum):
+            raise VitdecError("output buffer smaller than getOutputSize(inputNum)")
+        ms = ctypes.c_float(0.0)
+        _check(lib().vd_run(self._h, input_h.ctypes.data, output_h.ctypes.data, inputNum, ctypes.byref(ms)))
+        return output_h, ms.value
+
+    def run_device(self, input_ptr, output_ptr, inputNum, stream=0):
+        """Async device decode: raw device pointers on self.device, HIP stream handle (int)."""
+        _check(lib().vd_run_device(self._h, ctypes.c_void_p(input_ptr), ctypes.c_void_p(output_ptr), inputNum,
+                                   ctypes.c_void_p(stream)))
+
+
+def synth_device(options, n_bits, snr, seed, bits_ptr, packed_ptr, stream=0):
+    """GPU synthetic source: N-bit message -> packed channel input in device memory."""
+    _check(lib().vd_synth_device(options, n_bits, snr, seed, ctypes.c_void_p(bits_ptr) if bits_ptr else None,
+                                 ctypes.c_void_p(packed_ptr), ctypes.c_void_p(stream)))
+
+
+def simulate_host(options, n_bits, snr, bit_seed, noise_seed):
+    """Reference harness pipeline on the host (std::mt19937 + std::normal_distribution<float>)."""
+    bits = np.zeros(n_bits, dtype=np.uint8)
+    nbytes = lib().vd_input_size(options, 2 * n_bits)
+    packed = np.zeros(nbytes // 4, dtype=np.float32 if (options & CHANNEL_MASK) == FP32 else np.int32)
+    _check(lib().vd_simulate_host(options, n_bits, snr, bit_seed, noise_seed, bits.ctypes.data, packed.ctypes.data))
+    return bits, packed
+
+
+def count_errors(options, bits, decoded):
+    return int(lib().vd_count_errors(options, bits.ctypes.data, bits.size, decoded.ctypes.data, decoded.nbytes))
+
+
+def run_batches(options, inputs, inputNum, devices):
+    """Independent batches sharded over `devices` (vd_run_batches). Returns (outputs, wall ms)."""
+    n = len(inputs)
+    dt = np.uint16 if (options & DECODE_MASK) == O_B16 else np.uint32
+    outs = [np.zeros(lib().vd_output_size(options, inputNum) // np.dtype(dt).itemsize, dtype=dt) for _ in range(n)]
+    ins = (ctypes.c_void_p * n)(*[x.ctypes.data for x in inputs])
+    ous = (ctypes.c_void_p * n)(*[x.ctypes.data for x in outs])
+    devs = (ctypes.c_int * len(devices))(*devices)
+    ms = ctypes.c_float(0.0)
+    _check(lib().vd_run_batches(options, ins, ous, inputNum, n, devs, len(devices), ctypes.byref(ms)))
+    return outs, ms.value

@@ -1,0 +1,110 @@
+/*
+ * vd_capi.h -- C-ABI of the MI355X-native Viterbi decoder (K=7, R=1/2, polynomials 0171/0133).
+ *
+ * This is the drop-in boundary for the reference's decode path
+ * (alireza-md93/GPU-Accelerated-Viterbi-Decoder, class ViterbiCUDA<options>, src/viterbi/viterbi.h:43-152
+ * and src/viterbi/viterbi.cu:10-139,210-262).  Plain pointers and sizes only: no HIP, CUDA or torch
+ * types cross it.  include/viterbi.h rebuilds ViterbiCUDA<options> on top of these entry points;
+ * INTEGRATION.md shows the bindings (C++ header, ctypes) a maintainer adds.
+ *
+ * Option bitmask: identical encoding to the reference (viterbi.h:7-20):
+ *   channel  bits 0-3 : HARD=0 SOFT4=1 SOFT8=2 SOFT16=3 FP32=4
+ *   metric   bits 4-7 : M_B32=0x00 M_B16=0x10 M_FP16=0x20
+ *   output   bits 8-11: O_B32=0x000 O_B16=0x100
+ *   compMode bits 12-15: REG=0x0000 DPX=0x1000  (DPX decodes identically to REG: the reference never
+ *                        forwards compMode to its ACS, viterbi.cu:181,192,204)
+ *
+ * Status codes: every entry point that can fail returns an int (VD_OK = 0, negative on error) and
+ * records a message readable with vd_last_error().  The header-only ViterbiCUDA wrapper maps a
+ * non-zero status to stderr + exit(EXIT_FAILURE), the reference's HANDLE_ERROR behaviour
+ * (gpuerrors.h:8-17).
+ */
+#ifndef VD_CAPI_H
+#define VD_CAPI_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define VD_OK 0
+#define VD_ERR_OPTIONS (-1)   /* option combination disabled by OptionsValid (viterbi.h:22-41) */
+#define VD_ERR_ARG (-2)       /* null handle/pointer, or inputNum too small (< 128 encoded values) */
+#define VD_ERR_DEVICE (-3)    /* HIP runtime error (message in vd_last_error) */
+#define VD_ERR_NOMEM (-4)     /* device or pinned allocation failed */
+#define VD_ERR_NOKERNEL (-5)  /* the gfx950 code object is missing from this build */
+
+typedef struct vd_decoder vd_decoder;
+
+/* ---- option / size helpers (replace ViterbiCUDA::getInputSize/getMessageLen/getOutputSize,
+ *      viterbi.cu:63-92; sizes in bytes except vd_message_len, which is in decoded bits) ---- */
+
+/* 1 when OptionsValid<options>::value is true (viterbi.h:22-41), else 0 */
+int vd_options_valid(int options);
+/* bytes of packed channel input for inputNum encoded values (getInputSize, viterbi.cu:63-84) */
+size_t vd_input_size(int options, size_t inputNum);
+/* decoded bits produced (getMessageLen, viterbi.cu:86-88); 0 when inputNum < 128 */
+size_t vd_message_len(int options, size_t inputNum);
+/* bytes of decoded output (getOutputSize, viterbi.cu:90-92) */
+size_t vd_output_size(int options, size_t inputNum);
+/* number of independent stream chunks the decode is partitioned into (6400, viterbi.cu:19) */
+int vd_num_chunks(void);
+
+/* ---- decoder objects (replace ViterbiCUDA() / ViterbiCUDA(size_t) / ~ViterbiCUDA,
+ *      viterbi.cu:23-42,44-61) ---- */
+
+/* Create a decoder for `options` on HIP device `device` (the reference hard-codes device 0,
+ * viterbi.cu:132-139).  preallocInputNum > 0 reserves device buffers for that many encoded values,
+ * so later runs of that size or smaller allocate nothing (the reference's pre-allocating
+ * constructor, with the leak of viterbi.cu:31-36 fixed). */
+int vd_create(int options, size_t preallocInputNum, int device, vd_decoder** out);
+int vd_destroy(vd_decoder* dec);
+
+/* Blocking host-to-host decode (replaces ViterbiCUDA::run, viterbi.cu:210-238): copies
+ * vd_input_size(options, inputNum) bytes from input_h, decodes, copies vd_output_size bytes to
+ * output_h.  kernel_ms (optional) receives the decode-kernel time in ms measured with HIP events,
+ * the same scope as the reference's kernelTime (viterbi.cu:224-232). */
+int vd_run(vd_decoder* dec, const void* input_h, void* output_h, size_t inputNum, float* kernel_ms);
+
+/* Asynchronous device-to-device decode on `stream` (a hipStream_t passed as void*, NULL = the
+ * null stream).  input_d / output_d are device pointers on the decoder's device, sized as above.
+ * No allocation, no synchronisation: safe to capture in a hipGraph. */
+int vd_run_device(vd_decoder* dec, const void* input_d, void* output_d, size_t inputNum, void* stream);
+
+/* Batch sharding over several devices of one node: batch b (input_h[b] -> output_h[b],
+ * each inputNum encoded values) is decoded by devices[b % ndev]; batches are independent, so the
+ * result of each is identical to a single-device vd_run of that batch.  wall_ms (optional) is the
+ * wall time from first H2D to last D2H. */
+int vd_run_batches(int options, const void* const* input_h, void* const* output_h, size_t inputNum,
+                   int nbatches, const int* devices, int ndev, float* wall_ms);
+
+/* ---- synthetic channel source on the GPU (the reference's RandBitGen | ConvolutionalEncoder |
+ *      AddNoise | SoftDecisionPacker chain, viterbiDF.h:20-167, is host-side; this is the
+ *      product's own device-resident generator for benchmarks: bits from a counter-based hash,
+ *      not the reference's mt19937 stream) ---- */
+
+/* Fill bits_d (N bytes, 0/1) and the packed channel input packed_d (vd_input_size(options, 2N)
+ * bytes) for an N-bit message at `snr` (reference scaling: sigma = 10^(-snr/5), quantiser scale
+ * 40000).  N must be a multiple of 16.  Deterministic in `seed`. */
+int vd_synth_device(int options, size_t N, float snr, uint64_t seed, void* bits_d, void* packed_d,
+                    void* stream);
+
+/* Host-side reference-harness generator (std::mt19937 bits + std::normal_distribution<float>
+ * noise, exactly the reference pipeline's semantics, viterbiDF.h:20-167, main.cpp:131-137). */
+int vd_simulate_host(int options, size_t N, float snr, uint32_t bitSeed, uint32_t noiseSeed,
+                     uint8_t* bits, void* packed);
+/* bit-error count of a decoded buffer against the source bits (main.cpp:151-171) */
+long long vd_count_errors(int options, const uint8_t* bits, size_t N, const void* decoded, size_t decodedBytes);
+
+/* ---- runtime info ---- */
+const char* vd_last_error(void);
+int vd_device_count(void);
+/* last decode kernel's name and grid, for profilers (static strings) */
+const char* vd_kernel_name(int options);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* VD_CAPI_H */

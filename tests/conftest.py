@@ -1,0 +1,42 @@
+"""Shared test setup: import paths, the `gpu` marker, lazy oracle/product handles.
+
+Parity tests compare the HIP product (gpu-accelerated-viterbi-decoder_amd/lib/libvitdec.so via
+vitdec.py) with the CPU oracle (oracle/, test infrastructure only) on identical inputs.
+"""
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(ROOT, "gpu-accelerated-viterbi-decoder_amd")
+ORACLE = os.path.join(ROOT, "oracle")
+for p in (PKG, ORACLE):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (run on the GPU box)")
+    config.addinivalue_line("markers", "slow: full-size (32M-bit) cases")
+
+
+@pytest.fixture(scope="session")
+def vo():
+    import vd_oracle
+    vd_oracle.lib()
+    return vd_oracle
+
+
+@pytest.fixture(scope="session")
+def vd():
+    import vitdec
+    vitdec.lib()
+    return vitdec
+
+
+@pytest.fixture(scope="session")
+def gpu(vd):
+    if vd.device_count() < 1:
+        pytest.fail("gpu test but no HIP device visible (there is no CPU fallback)")
+    return vd
