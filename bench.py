@@ -1,0 +1,207 @@
+#!/usr/bin/env python3
+"""Benchmark: decoded Gb/s at K=7 R=1/2, 32M bits, hard + soft8 (BASELINE.json metric).
+
+One step = one pass of the decode hot path over one batch of each headline workload, inputs
+already resident in HBM:
+  * HARD  input, int32 metric core   (BASELINE configs[1]: 32M bits, `-i h -m b32`)
+  * SOFT8 input, int16x2 metric core (BASELINE configs[2]: 32M bits, `-i s8 -m b16`)
+value = decoded bits of both batches (2 x getMessageLen(64e6) = 63,999,872) / step time, summed
+over ranks.  Multi-GPU (BASELINE configs[3]): one process per GPU, each rank decodes its own
+independent batches (weak scaling, no data-path collective; an RCCL all_gather of per-rank
+checksums runs once after the timed region).
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
+   or: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "gpu-accelerated-viterbi-decoder_amd"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import vitdec  # noqa: E402
+
+N_BITS = 32_000_000
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md)
+SNR_DB = 2.0
+
+WORKLOADS = [
+    ("hard_b32", vitdec.HARD | vitdec.M_B32 | vitdec.O_B32),
+    ("soft8_b16", vitdec.SOFT8 | vitdec.M_B16 | vitdec.O_B32),
+]
+
+
+def algorithmic_bytes(opt, input_num):
+    """HBM bytes a decode must move: packed channel input + packed decoded output."""
+    return vitdec.lib().vd_input_size(opt, input_num) + vitdec.lib().vd_output_size(opt, input_num)
+
+
+def cpu_baseline(sample_bits=2_000_000):
+    """Scalar host Viterbi (the oracle's CPU restatement, 1 thread) on a bounded sample."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import vd_oracle as vo
+    opt = WORKLOADS[0][1]
+    _, packed = vo.simulate(opt, sample_bits, SNR_DB, 1, 2)
+    t0 = time.perf_counter()
+    out, _ = vo.decode(opt, packed, nthreads=1)
+    dt = time.perf_counter() - t0
+    bits = vo.message_len(opt, 2 * sample_bits)
+    return {"value": round(bits / dt / 1e9, 6), "unit": "Gb/s", "cores": 1, "kind": "port",
+            "sample": f"HARD int32-metric decode of a {sample_bits // 1_000_000}M-bit message (1/16 of the "
+                      f"32M batch, same 6400-chunk partition), oracle/vd_oracle.c on 1 host thread, {dt:.1f} s"}
+
+
+def load_traffic():
+    """HBM bytes per launch from the committed rocprofv3 PMC summary (profiles/), if present."""
+    p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if os.path.exists(p):
+        with open(p) as f:
+            return json.load(f)
+    return {}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.cuda.current_device()
+    stream = torch.cuda.current_stream()
+    sptr = stream.cuda_stream
+
+    # resident inputs: each rank synthesises its own independent batches in HBM
+    batches = []
+    for wi, (name, opt) in enumerate(WORKLOADS):
+        input_num = 2 * N_BITS
+        nin = vitdec.lib().vd_input_size(opt, input_num)
+        nout = vitdec.lib().vd_output_size(opt, input_num)
+        inp = torch.empty(nin, dtype=torch.uint8, device=dev)
+        bits = torch.empty(N_BITS, dtype=torch.uint8, device=dev)
+        out = torch.empty(nout, dtype=torch.uint8, device=dev)
+        vitdec.synth_device(opt, N_BITS, SNR_DB, 1000 * rank + wi + 1, bits.data_ptr(), inp.data_ptr(), sptr)
+        dec = vitdec.ViterbiCUDA(opt, 0, dev)
+        batches.append(dict(name=name, opt=opt, input_num=input_num, inp=inp, out=out, bits=bits, dec=dec,
+                            msg=vitdec.lib().vd_message_len(opt, input_num)))
+    torch.cuda.synchronize()
+
+    nw = len(batches)
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(nw + 1)] for _ in range(args.steps)]
+
+    def step(ev=None):
+        if ev is not None:
+            ev[0].record(stream)
+        for i, b in enumerate(batches):
+            b["dec"].run_device(b["inp"].data_ptr(), b["out"].data_ptr(), b["input_num"], sptr)
+            if ev is not None:
+                ev[i + 1].record(stream)
+
+    for _ in range(args.warmup):
+        step()
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for s in range(args.steps):
+        step(evs[s])
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    elapsed = time.perf_counter() - t0
+
+    # per-kernel average durations from HIP events on the launch stream
+    kms = [float(np.mean([evs[s][i].elapsed_time(evs[s][i + 1]) for s in range(args.steps)])) for i in range(nw)]
+
+    # correctness side-channel (outside the timed region): BER of each batch vs its source bits,
+    # and an RCCL all_gather of per-rank decoded-word checksums (the only cross-GPU traffic)
+    bers = []
+    sums = []
+    for b in batches:
+        bits_h = b["bits"].cpu().numpy()
+        dt = np.uint16 if (b["opt"] & 0xF00) == vitdec.O_B16 else np.uint32
+        out_h = b["out"].cpu().numpy().view(dt)
+        bers.append(vitdec.count_errors(b["opt"], bits_h, out_h) / b["msg"])
+        sums.append(int(np.bitwise_xor.reduce(out_h.view(np.uint32))))
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        elapsed = float(t.item())
+        cs = torch.tensor(sums, dtype=torch.int64, device=dev)
+        gathered = [torch.empty_like(cs) for _ in range(world)]
+        torch.distributed.all_gather(gathered, cs)
+
+    if rank == 0:
+        bits_per_step = sum(b["msg"] for b in batches)
+        ms_per_step = elapsed / args.steps * 1e3
+        value = bits_per_step * world * args.steps / elapsed / 1e9
+        # dominant kernel roofline (HBM, algorithmic bytes = packed input + packed output)
+        di = int(np.argmax(kms))
+        db = batches[di]
+        alg = algorithmic_bytes(db["opt"], db["input_num"])
+        achieved = alg / (kms[di] * 1e-3) / 1e9
+        traffic = load_traffic().get(db["name"])
+        result = {
+            "metric": "decoded Gb/s at K=7 R=1/2, 32M bits, hard+soft8",
+            "value": round(value, 3),
+            "unit": "Gb/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "int32+int16x2",
+            "data": f"synthetic: GPU counter-hash bits, K=7 (0171,0133) encoder, BPSK+AWGN at {SNR_DB} dB, "
+                    f"quantiser scale 40000 (reference harness scaling)",
+            "config": {
+                "workload": "per GPU per step: one 32M-bit HARD batch on the int32 core + one 32M-bit SOFT8 "
+                            "batch on the int16x2 core (BASELINE configs[1]+[2]); each batch uses the "
+                            "reference's 6400-chunk partition",
+                "n_bits_per_batch": N_BITS,
+                "decoded_bits_per_batch": batches[0]["msg"],
+                "parallelism": f"batch-shard x{world}" if world > 1 else "single GPU",
+                "kernel_ms": {b["name"]: round(k, 4) for b, k in zip(batches, kms)},
+                "kernel_gbps": {b["name"]: round(b["msg"] / (k * 1e-3) / 1e9, 2) for b, k in zip(batches, kms)},
+                "ber": {b["name"]: bers[i] for i, b in enumerate(batches)},
+                "kernels": {b["name"]: vitdec.kernel_name(b["opt"]) for b in batches},
+            },
+            "roofline": {
+                "bound": "hbm",
+                "kernel": db["name"] + ": " + vitdec.kernel_name(db["opt"]),
+                "achieved": round(achieved, 2),
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 5),
+                "traffic": traffic,
+                "algorithmic_bytes_per_launch": alg,
+            },
+        }
+        if not args.no_cpu_baseline and world == 1:
+            result["cpu_baseline"] = cpu_baseline()
+        print(json.dumps(result), flush=True)
+
+    for b in batches:
+        b["dec"].close()
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

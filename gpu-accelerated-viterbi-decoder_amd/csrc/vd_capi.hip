@@ -94,10 +94,8 @@ using launch_fn = void (*)(const void*, void*, vd::Geom, hipStream_t);
 template <int CH, int CORE, int OB>
 void launch_t(const void* in, void* out, vd::Geom g, hipStream_t s)
 {
-    if constexpr (CORE == vd::B32)
-        hipLaunchKernelGGL((vd::vd_decode_b32<CH, OB>), dim3(g.nchunks), dim3(64), 0, s, in, out, g);
-    else
-        hipLaunchKernelGGL((vd::vd_decode_pk<CH, CORE, OB>), dim3((g.nchunks + 1) / 2), dim3(64), 0, s, in, out, g);
+    hipLaunchKernelGGL((vd::vd_decode_sc<CH, CORE, OB>), dim3((g.nchunks + vd::kWaves - 1) / vd::kWaves),
+                       dim3(64 * vd::kWaves), 0, s, in, out, g);
 }
 
 template <int CH, int CORE>
@@ -122,11 +120,11 @@ launch_fn pick(int o)
 const char* kname(int o)
 {
     static const char* names[5][3] = {
-        {"vd_decode_b32<HARD>", "vd_decode_pk<HARD,B16>", "vd_decode_pk<HARD,F16>"},
-        {"vd_decode_b32<SOFT4>", "vd_decode_pk<SOFT4,B16>", "vd_decode_pk<SOFT4,F16>"},
-        {"vd_decode_b32<SOFT8>", "vd_decode_pk<SOFT8,B16>", "-"},
-        {"vd_decode_b32<SOFT16>", "-", "-"},
-        {"vd_decode_b32<FP32>", "vd_decode_pk<FP32,B16>", "vd_decode_pk<FP32,F16>"},
+        {"vd_decode_sc<HARD,B32>", "vd_decode_sc<HARD,B16>", "vd_decode_sc<HARD,F16>"},
+        {"vd_decode_sc<SOFT4,B32>", "vd_decode_sc<SOFT4,B16>", "vd_decode_sc<SOFT4,F16>"},
+        {"vd_decode_sc<SOFT8,B32>", "vd_decode_sc<SOFT8,B16>", "-"},
+        {"vd_decode_sc<SOFT16,B32>", "-", "-"},
+        {"vd_decode_sc<FP32,B32>", "vd_decode_sc<FP32,B16>", "vd_decode_sc<FP32,F16>"},
     };
     if (!valid(o)) return "-";
     return names[ch_of(o)][met_of(o)];

@@ -13,7 +13,8 @@
 //    two chunks per wave, chunk 2w in the low and chunk 2w+1 in the high half of every lane, so one
 //    v_pk_add/v_pk_sub/v_pk_max advances two chunks.
 //  * Survivors.  No register exchange: each stage's decision ("took the exchanged predecessor") is
-//    shifted into a per-lane 32-bit word; one word per lane per 32-stage block goes to an LDS ring.
+//    the sign bit of a candidate difference, shifted into per-lane words with pure-VGPR ops; one
+//    word per lane per 32-stage block (int32) or per 16-stage half-block (packed) goes to an LDS ring.
 //    Output words are traced back lane-parallel (TB words at a time) in POSITION space, where a
 //    traceback step is p ^= d << q -- no state arithmetic.
 //  * Branch metrics.  Per 32-stage block, 32 lanes compute the 4 branch metrics of one stage each
@@ -66,10 +67,11 @@ __device__ __forceinline__ int own_label(int p, int k)
 }
 
 // xor-lane exchange along position bit Q (see header)
-template <int Q>
+template <int Q, int ABL = 0>
 __device__ __forceinline__ int xchg(int x, int bp_addr)
 {
-    if constexpr (Q == 0) return __builtin_amdgcn_mov_dpp(x, 0xB1, 0xF, 0xF, true);   // quad_perm 1,0,3,2
+    if constexpr ((ABL & 2) && Q >= 4) return __builtin_amdgcn_mov_dpp(x, 0x124, 0xF, 0xF, true);
+    else if constexpr (Q == 0) return __builtin_amdgcn_mov_dpp(x, 0xB1, 0xF, 0xF, true);   // quad_perm 1,0,3,2
     else if constexpr (Q == 1) return __builtin_amdgcn_mov_dpp(x, 0x4E, 0xF, 0xF, true);  // quad_perm 2,3,0,1
     else if constexpr (Q == 2) {
         int y = __builtin_amdgcn_mov_dpp(x, 0x141, 0xF, 0xF, true);  // row_half_mirror: i -> 7-i
@@ -79,54 +81,31 @@ __device__ __forceinline__ int xchg(int x, int bp_addr)
     else return __builtin_amdgcn_ds_bpermute(bp_addr, x);                     // lane ^ 32
 }
 
-// ---------------------------------------------------------------- decision accumulation
-// acc = 2*acc + (a CMP b): the compare lands in VCC and v_addc_co_u32 shifts it in as the carry, one
-// VALU op per decision instead of the select/or/shift sequence the compiler builds otherwise.
-__device__ __forceinline__ uint32_t dec_ge_i32(uint32_t acc, int a, int b)
-{
-    asm("v_cmp_ge_i32 vcc, %1, %2\n\tv_addc_co_u32 %0, vcc, %0, %0, vcc" : "+v"(acc) : "v"(a), "v"(b) : "vcc");
-    return acc;
-}
-// low halves (int16)
-__device__ __forceinline__ uint32_t dec_ge_i16lo(uint32_t acc, uint32_t a, uint32_t b)
-{
-    asm("v_cmp_ge_i16 vcc, %1, %2\n\tv_addc_co_u32 %0, vcc, %0, %0, vcc" : "+v"(acc) : "v"(a), "v"(b) : "vcc");
-    return acc;
-}
-// high halves (int16), read through SDWA word selects
-__device__ __forceinline__ uint32_t dec_ge_i16hi(uint32_t acc, uint32_t a, uint32_t b)
-{
-    asm("v_cmp_ge_i16_sdwa vcc, %1, %2 src0_sel:WORD_1 src1_sel:WORD_1\n\tv_addc_co_u32 %0, vcc, %0, %0, vcc"
-        : "+v"(acc) : "v"(a), "v"(b) : "vcc");
-    return acc;
-}
-__device__ __forceinline__ uint32_t dec_gt_f16lo(uint32_t acc, uint32_t a, uint32_t b)
-{
-    asm("v_cmp_gt_f16 vcc, %1, %2\n\tv_addc_co_u32 %0, vcc, %0, %0, vcc" : "+v"(acc) : "v"(a), "v"(b) : "vcc");
-    return acc;
-}
-__device__ __forceinline__ uint32_t dec_gt_f16hi(uint32_t acc, uint32_t a, uint32_t b)
-{
-    asm("v_cmp_gt_f16_sdwa vcc, %1, %2 src0_sel:WORD_1 src1_sel:WORD_1\n\tv_addc_co_u32 %0, vcc, %0, %0, vcc"
-        : "+v"(acc) : "v"(a), "v"(b) : "vcc");
-    return acc;
-}
-
+// ---------------------------------------------------------------- decision bits
+// A stage's decision is the sign of a candidate difference, shifted into a per-lane word with pure
+// VGPR ops (v_alignbit_b32 / v_pk_lshrrev_b16 + v_bfi_b32).  Routing it through VCC (v_cmp + v_addc)
+// was measured 2.6x slower on gfx950: the VALU->SGPR->VALU dependency serialises every stage.
 // ---------------------------------------------------------------- channel input -> branch metrics
 // For stage g: A = BM[label 3] = s0+s1 and B = BM[label 2] = s0-s1 (BM[0] = -A, BM[1] = -B).
 // Reference: viterbiBM.cuh:15-153 (formats), viterbi.h:80-87 (values per 32-bit word).
 template <int CH>
 struct In;
 
+// Loads are unconditional (clamped address) so the compiler can count them with vmcnt(N) across
+// the prefetch distance; stages past the input (only reachable by the O_B16 overrun and by the
+// shorter chunk of a packed pair) read as zero words in ab().
+__device__ __forceinline__ uint64_t clampg(uint64_t g, uint64_t avail) { return g < avail ? g : avail - 1; }
+
 template <>
 struct In<HARD> {  // 16 stages per word, stage g -> bits 31-2(g%16) (s0) and 30-2(g%16) (s1)
     using raw_t = uint32_t;
     static __device__ __forceinline__ raw_t load(const void* p, uint64_t g, uint64_t avail)
     {
-        return g < avail ? __builtin_nontemporal_load(&((const uint32_t*)p)[g >> 4]) : 0u;
+        return __builtin_nontemporal_load(&((const uint32_t*)p)[clampg(g, avail) >> 4]);
     }
-    static __device__ __forceinline__ void ab(raw_t w, uint64_t g, int& A, int& B)
+    static __device__ __forceinline__ void ab(raw_t w, uint64_t g, uint64_t avail, int& A, int& B)
     {
+        w = g < avail ? w : 0u;
         int sh = 30 - 2 * (int)(g & 15);
         int r0 = (w >> (sh + 1)) & 1, r1 = (w >> sh) & 1;
         A = r0 + r1 - 1;  // 1 - #mismatches against (1,1)
@@ -138,10 +117,11 @@ struct In<SOFT4> {  // 4 stages per word, byte g%4 from the MSB: high nibble s0,
     using raw_t = uint32_t;
     static __device__ __forceinline__ raw_t load(const void* p, uint64_t g, uint64_t avail)
     {
-        return g < avail ? __builtin_nontemporal_load(&((const uint32_t*)p)[g >> 2]) : 0u;
+        return __builtin_nontemporal_load(&((const uint32_t*)p)[clampg(g, avail) >> 2]);
     }
-    static __device__ __forceinline__ void ab(raw_t w, uint64_t g, int& A, int& B)
+    static __device__ __forceinline__ void ab(raw_t w, uint64_t g, uint64_t avail, int& A, int& B)
     {
+        w = g < avail ? w : 0u;
         int sh = 24 - 8 * (int)(g & 3);
         int s0 = (int)(w << (24 - sh)) >> 28;
         int s1 = (int)(w << (28 - sh)) >> 28;
@@ -154,10 +134,12 @@ struct In<SOFT8> {  // 2 stages per word; the 16-bit half (g^1) holds s0 (high b
     using raw_t = uint32_t;
     static __device__ __forceinline__ raw_t load(const void* p, uint64_t g, uint64_t avail)
     {
-        return g < avail ? (uint32_t)__builtin_nontemporal_load(&((const uint16_t*)p)[g ^ 1]) : 0u;
+        uint64_t c = clampg(g, avail);
+        return (uint32_t)__builtin_nontemporal_load(&((const uint16_t*)p)[c ^ 1]);
     }
-    static __device__ __forceinline__ void ab(raw_t w, uint64_t, int& A, int& B)
+    static __device__ __forceinline__ void ab(raw_t w, uint64_t g, uint64_t avail, int& A, int& B)
     {
+        w = g < avail ? w : 0u;
         int s0 = (int)(w << 16) >> 24;
         int s1 = (int)(w << 24) >> 24;
         A = s0 + s1;
@@ -169,10 +151,11 @@ struct In<SOFT16> {  // 1 stage per word: high 16 bits s0, low 16 bits s1
     using raw_t = uint32_t;
     static __device__ __forceinline__ raw_t load(const void* p, uint64_t g, uint64_t avail)
     {
-        return g < avail ? __builtin_nontemporal_load(&((const uint32_t*)p)[g]) : 0u;
+        return __builtin_nontemporal_load(&((const uint32_t*)p)[clampg(g, avail)]);
     }
-    static __device__ __forceinline__ void ab(raw_t w, uint64_t, int& A, int& B)
+    static __device__ __forceinline__ void ab(raw_t w, uint64_t g, uint64_t avail, int& A, int& B)
     {
+        w = g < avail ? w : 0u;
         int s0 = (int)w >> 16;
         int s1 = (int)(w << 16) >> 16;
         A = s0 + s1;
@@ -185,11 +168,12 @@ struct In<FP32> {  // 2 floats per stage, clamped to [-8,7]; BM = (int)(+-x0 +- 
     static __device__ __forceinline__ raw_t load(const void* p, uint64_t g, uint64_t avail)
     {
         typedef float f2 __attribute__((ext_vector_type(2)));
-        f2 v = g < avail ? __builtin_nontemporal_load(&((const f2*)p)[g]) : f2{0.f, 0.f};
+        f2 v = __builtin_nontemporal_load(&((const f2*)p)[clampg(g, avail)]);
         return make_float2(v.x, v.y);
     }
-    static __device__ __forceinline__ void ab(raw_t v, uint64_t, int& A, int& B)
+    static __device__ __forceinline__ void ab(raw_t v, uint64_t g, uint64_t avail, int& A, int& B)
     {
+        if (g >= avail) v = make_float2(0.f, 0.f);
         float x0 = fminf(fmaxf(v.x, -8.0f), 7.0f);
         float x1 = fminf(fmaxf(v.y, -8.0f), 7.0f);
         A = (int)__fadd_rn(x0, x1);
@@ -214,11 +198,17 @@ __device__ __forceinline__ ChunkRange chunk_range(const Geom& g, uint32_t c)
 
 // ---------------------------------------------------------------- lane-parallel traceback
 // Lane traces output word k (0-based within its chunk); block k+2 sits in ring slot l+1, block k+1
-// in slot l (slots of slotB bytes, this chunk's 64 decision words at chunkOffB inside a slot).
-// Position-space traceback: p_{t-1} = p_t ^ (d_t(p_t) << q_t); the decoded bit of stage t is bit
-// q_t of p_{t-1} (the dropped bit of the predecessor state).  Reference: viterbiTB.cuh:4-21.
-__device__ __forceinline__ uint32_t traceback_word(const char* ring, int slotB, int chunkOffB, int l, uint64_t k)
+// in slot l.  Position-space traceback: p_{t-1} = p_t ^ (d_t(p_t) << q_t); the decoded bit of stage t
+// is bit q_t of p_{t-1} (the dropped bit of the predecessor state).  Reference: viterbiTB.cuh:4-21.
+// Ring formats:
+//   PK=false (int32 core): slot = 64 words (lane p), bit 31-s = decision of stage s of the block.
+//   PK=true  (packed cores): slot = 2 half-blocks x 64 words; half-block hb holds stages 16hb..16hb+15,
+//            the low 16 bits for the chunk in the low metric halves, the high 16 bits for the other;
+//            bit s' of a 16-bit half = stage 16hb+s'.  `Q` carries 2h (byte select of the half).
+template <bool PK>
+__device__ __forceinline__ uint32_t traceback_word(const char* ring, int h, int l, uint64_t k)
 {
+    constexpr int SLOTB = PK ? 512 : 256;
     const int e6 = (int)((95 + 32 * k) % 6);  // stage phase of the traceback start
     int MK[6], QS[6];
     sfor<6>([&](auto R) {
@@ -228,34 +218,74 @@ __device__ __forceinline__ uint32_t traceback_word(const char* ring, int slotB, 
         MK[r] = 4 << q;
         QS[r] = q + 2;
     });
-    uint32_t Q = (uint32_t)((l + 1) * slotB + chunkOffB);  // position 0 = state 0
-    sfor<32>([&](auto I) {
-        constexpr int i = decltype(I)::value;
-        uint32_t w = *(const uint32_t*)(ring + Q);
-        int d = (int)(w << (31 - i)) >> 31;  // bit i = stage 31-i of the block (stage 95+32k-i)
-        Q ^= (uint32_t)(d & MK[i % 6]);
-    });
-    Q -= (uint32_t)slotB;
+    uint32_t Q = (uint32_t)((l + 1) * SLOTB + (PK ? 2 * h : 0));  // position 0 = state 0
     uint32_t word = 0;
-    sfor<32>([&](auto I) {
+    sfor<64>([&](auto I) {
         constexpr int i = decltype(I)::value;
-        uint32_t w = *(const uint32_t*)(ring + Q);
-        int d = (int)(w << (31 - i)) >> 31;
-        Q ^= (uint32_t)(d & MK[(i + 32) % 6]);
-        word |= ((Q >> QS[(i + 32) % 6]) & 1u) << i;  // word bit i <-> stage 63+32k-i
+        constexpr int s = 31 - (i & 31);  // stage within the block
+        int d;
+        if constexpr (PK) {
+            constexpr int off = (s >> 4) * 256;
+            uint32_t w = *(const uint16_t*)(ring + Q + off);
+            d = (int)(w << (31 - (s & 15))) >> 31;
+        } else {
+            uint32_t w = *(const uint32_t*)(ring + Q);
+            d = (int)(w << s) >> 31;
+        }
+        Q ^= (uint32_t)(d & MK[i % 6]);
+        if constexpr (i == 31) Q -= (uint32_t)SLOTB;
+        if constexpr (i >= 32) word |= ((Q >> QS[i % 6]) & 1u) << (i - 32);  // word bit <-> stage 63+32k-(i-32)
     });
     return word;
 }
 
-// ================================================================ int32 core: one chunk per wave
-template <int CH, int OB>
-__global__ __launch_bounds__(64) void vd_decode_b32(const void* __restrict__ in, void* __restrict__ out, Geom geo)
+// ================================================================ fp32 core: one chunk per wave
+// Every metric core (M_B32, M_B16, M_FP16) runs here in exact-integer fp32: branch metrics are
+// integers of magnitude <= 65534, path metrics stay below 2^22 after the per-block renormalisation,
+// so fp32 add/sub/max are exact and the decisions equal the reference's int32/int16/fp16 ones; the
+// metric type only selects the tie rule.  fp32 because on gfx950 v_add/v_sub/v_fma_f32 issue every
+// 2 cycles per wave64 while v_max, DPP, v_pk_* and integer shift/bitfield ops take 4 (tools/vd_ubench).
+// Per stage: t1 = own + m, t2 = exchanged - m (DPP-fused or LDS permute), pm = max(t1, t2),
+// bit = clamp(t1 - t2) (a 0.0/1.0 from v_sub_f32's clamp modifier), acc = fma(acc, 2, bit).
+template <int CORE>
+struct Tie;
+// bit = NOT take (t1 > t2 strictly) : exchanged wins ties
+template <> struct Tie<B16> { static constexpr bool kInvert = true; };
+template <> struct Tie<B32> { static constexpr bool kInvert = true; };
+// bit = take (t2 > t1 strictly) : own wins ties
+template <> struct Tie<F16> { static constexpr bool kInvert = false; };
+
+__device__ __forceinline__ float clamp01(float x) { return __builtin_amdgcn_fmed3f(x, 0.0f, 1.0f); }
+
+template <int Q, int ABL = 0>
+__device__ __forceinline__ float xchgf(float x, int bp_addr)
+{
+    return __builtin_bit_cast(float, xchg<Q, ABL>(__builtin_bit_cast(int, x), bp_addr));
+}
+
+// Workgroups of kWaves independent waves (one chunk each): gfx950 admits a bounded number of
+// workgroups per CU, so single-wave workgroups could not keep all 6400 chunks resident at once.
+// Waves never synchronise with each other; LDS is partitioned per wave and wave_sync() only orders
+// the wave's own LDS traffic (LDS instructions of one wave execute in order).
+constexpr int kWaves = 4;
+__device__ __forceinline__ void wave_sync()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+template <int CH, int CORE, int OB, int ABL = 0>
+__global__ __launch_bounds__(64 * kWaves) void vd_decode_sc(const void* __restrict__ in, void* __restrict__ out, Geom geo)
 {
     using IN = In<CH>;
-    __shared__ int4 tab[32];                     // per stage: BM[0..3]
-    __shared__ uint32_t ring[(kTB + 1) * 64];    // decision words, 64 per 32-stage block
-    const int lane = threadIdx.x;
-    const ChunkRange cr = chunk_range(geo, blockIdx.x);
+    __shared__ float4 tab_all[kWaves][96];                   // per stage of a 3-block group: BM[0..3]
+    __shared__ uint32_t ring_all[kWaves][(kTB + 1) * 64];    // per block: 64 words, bit 31-s = stage s
+    const int lane = threadIdx.x & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    float4* tab = tab_all[wv];
+    uint32_t* ring = ring_all[wv];
+    const ChunkRange cr = chunk_range(geo, blockIdx.x * kWaves + wv);
     if (cr.words == 0) return;
     const uint64_t start = cr.startWord * OB;                      // first stage of the chunk
     const uint32_t S = OB == 32 ? cr.words : (cr.words + 1) / 2;  // 32-bit words traced back
@@ -266,53 +296,55 @@ __global__ __launch_bounds__(64) void vd_decode_b32(const void* __restrict__ in,
         constexpr int k = decltype(K)::value;
         L4[k] = own_label(lane, k) * 4;
     });
-    const int ebias = lane >= 32 ? 1 : 0;  // M_B32, t%6==0: lanes with p5=1 keep own on ties
+    // M_B32 at t%6==0: lanes >= 32 (position bit 5 = 1) keep their own predecessor on ties
+    const float ebias = (CORE == B32 && lane >= 32) ? 1.0f : 0.0f;
     const int bp_addr = (lane ^ 32) * 4;
-    const int* tabi = (const int*)tab;
+    const float* tabf = (const float*)tab;
+    const uint64_t avail = geo.availStages;
+    const uint64_t li = (uint64_t)(lane & 31);
 
-    int pm = 0;
-    uint32_t acc = 0;
+    float pm = 0.0f;
     uint32_t kb = 0;
-    typename IN::raw_t raw = IN::load(in, start + (uint64_t)(lane & 31), geo.availStages);
+    // Input of a 3-block group is loaded one group ahead (~96 stages of compute, several loaded-HBM
+    // round trips) and turned into the group's branch-metric table at the head of the group.
+    typename IN::raw_t rA = IN::load(in, start + li, avail);
+    typename IN::raw_t rB = IN::load(in, start + 32 + li, avail);
+    typename IN::raw_t rC = IN::load(in, start + 64 + li, avail);
 
-    for (uint32_t j = 0; j < nblk; j++) {
-        if (lane < 32) {
-            int A, B;
-            IN::ab(raw, start + 32ull * j + lane, A, B);
-            tab[lane] = make_int4(-A, -B, B, A);
-        }
-        if (j + 1 < nblk) raw = IN::load(in, start + 32ull * (j + 1) + (uint64_t)(lane & 31), geo.availStages);
-        __syncthreads();
-
-        auto run = [&](auto PHc) {
-            constexpr int PH = decltype(PHc)::value;
-            sfor<32>([&](auto I) {
-                constexpr int i = decltype(I)::value;
-                constexpr int K = (PH + i) % 6;
-                constexpr int Q = (K + 5) % 6;
-                const int m = tabi[i * 4 + (L4[K] >> 2)];
-                const int oth = xchg<Q>(pm, bp_addr);
-                const int t1 = pm + m, t2 = oth - m;
-                pm = t1 > t2 ? t1 : t2;  // the survivor value does not depend on the tie rule
-                if constexpr (K == 0) acc = dec_ge_i32(acc, t2 - t1, ebias);
-                else acc = dec_ge_i32(acc, t2, t1);
-            });
-        };
-        switch (j % 3) {
-        case 0: run(std::integral_constant<int, 0>{}); break;
-        case 1: run(std::integral_constant<int, 2>{}); break;
-        default: run(std::integral_constant<int, 4>{}); break;
-        }
-        // decision-neutral renormalisation: keeps |pm| small for SOFT16 over long chunks
-        pm -= __builtin_amdgcn_readfirstlane(pm);
-        __syncthreads();
-        if (j >= 1) ring[(j - 1 - kb) * 64 + lane] = acc;
+    // one 32-stage block j (stage phase 2j%6 = PH, table rows 32*TB0..); false after the last block
+    auto block = [&](auto PHc, uint32_t j) {
+        constexpr int PH = decltype(PHc)::value;
+        constexpr int TB0 = PH / 2;
+        float acc = 0.0f;
+        uint32_t hi16 = 0, word = 0;
+        sfor<32>([&](auto I) {
+            constexpr int i = decltype(I)::value;
+            constexpr int K = (PH + i) % 6;
+            constexpr int Q = (K + 5) % 6;
+            const float m = (ABL & 4) ? (float)L4[K] : tabf[(TB0 * 32 + i) * 4 + (L4[K] >> 2)];
+            const float oth = xchgf<Q, ABL>(pm, bp_addr);
+            const float t1 = pm + m, t2 = oth - m;
+            pm = fmaxf(t1, t2);  // the survivor value does not depend on the tie rule
+            float bit;
+            if constexpr (!Tie<CORE>::kInvert) bit = clamp01(t2 - t1);
+            else if constexpr (CORE == B32 && K == 0) bit = clamp01((t1 + ebias) - t2);
+            else bit = clamp01(t1 - t2);
+            if constexpr (ABL & 8) asm volatile("" ::"v"(bit));
+            else acc = (i == 0 || i == 16) ? bit : __builtin_fmaf(acc, 2.0f, bit);  // 16 bits per half
+            if constexpr (i == 15) hi16 = (uint32_t)acc;
+            if constexpr (i == 31) word = (hi16 << 16) | (uint32_t)acc;
+        });
+        // decision-neutral renormalisation by the metric of position 0 (keeps |pm| < 2^22)
+        pm -= __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, pm)));
+        if (Tie<CORE>::kInvert) word = ~word;  // ring holds take-bits
+        wave_sync();
+        if (j >= 1) ring[(j - 1 - kb) * 64 + lane] = word;
         if (j >= 2 && (j - 1 - kb == (uint32_t)kTB || j == nblk - 1)) {
-            __syncthreads();
+            wave_sync();
             const uint32_t nw = j - 1 - kb;  // words kb .. j-2
-            if ((uint32_t)lane < nw) {
+            if (!(ABL & 1) && (uint32_t)lane < nw) {
                 const uint64_t k = kb + lane;
-                uint32_t w = traceback_word((const char*)ring, 256, 0, lane, k);
+                uint32_t w = traceback_word<false>((const char*)ring, 0, lane, k);
                 if constexpr (OB == 32) {
                     ((uint32_t*)out)[cr.startWord + k] = w;
                 } else {
@@ -321,11 +353,34 @@ __global__ __launch_bounds__(64) void vd_decode_b32(const void* __restrict__ in,
                     if (2 * k + 1 < cr.words) o[2 * k + 1] = (uint16_t)(w & 0xFFFF);
                 }
             }
-            __syncthreads();
-            ring[lane] = acc;  // block j becomes slot 0 of the next batch
+            wave_sync();
+            ring[lane] = word;  // block j becomes slot 0 of the next batch
             kb = j - 1;
         }
+        return j + 1 < nblk;
+    };
+    for (uint32_t j = 0;; j += 3) {
+        if (lane < 32) {
+            int A, B;
+            IN::ab(rA, start + 32ull * j + li, avail, A, B);
+            tab[lane] = make_float4((float)-A, (float)-B, (float)B, (float)A);
+            IN::ab(rB, start + 32ull * (j + 1) + li, avail, A, B);
+            tab[32 + lane] = make_float4((float)-A, (float)-B, (float)B, (float)A);
+            IN::ab(rC, start + 32ull * (j + 2) + li, avail, A, B);
+            tab[64 + lane] = make_float4((float)-A, (float)-B, (float)B, (float)A);
+        }
+        if constexpr (!(ABL & 16)) {
+            rA = IN::load(in, start + 32ull * (j + 3) + li, avail);
+            rB = IN::load(in, start + 32ull * (j + 4) + li, avail);
+            rC = IN::load(in, start + 32ull * (j + 5) + li, avail);
+        }
+        wave_sync();
+        if (!block(std::integral_constant<int, 0>{}, j)) break;
+        if (!block(std::integral_constant<int, 2>{}, j + 1)) break;
+        if (!block(std::integral_constant<int, 4>{}, j + 2)) break;
+        wave_sync();  // this group's table reads complete before the next group overwrites it
     }
+    if constexpr (ABL & 8) asm volatile("" ::"v"(pm));
 }
 
 // ================================================================ packed cores: two chunks per wave
@@ -334,15 +389,15 @@ struct Pk;
 template <>
 struct Pk<B16> {
     typedef short v2 __attribute__((ext_vector_type(2)));
+    static constexpr bool kInvert = true;  // sign(t2 - t1) = NOT take: exchanged wins ties
     static __device__ __forceinline__ uint32_t cvt(int a) { return (uint32_t)(uint16_t)(int16_t)a; }
     static __device__ __forceinline__ v2 as(uint32_t x) { return __builtin_bit_cast(v2, x); }
     static __device__ __forceinline__ uint32_t bits(v2 x) { return __builtin_bit_cast(uint32_t, x); }
-    // one ACS for both halves; exchanged predecessor wins ties (viterbiACS.cuh:113-119,216-220)
-    static __device__ __forceinline__ uint32_t acs(uint32_t own, uint32_t oth, uint32_t m, uint32_t& a0, uint32_t& a1)
+    // one ACS for both halves (viterbiACS.cuh:113-119,216-220); d carries the decision in the sign bits
+    static __device__ __forceinline__ uint32_t acs(uint32_t own, uint32_t oth, uint32_t m, uint32_t& d)
     {
         v2 t1 = as(own) + as(m), t2 = as(oth) - as(m);
-        a0 = dec_ge_i16lo(a0, bits(t2), bits(t1));
-        a1 = dec_ge_i16hi(a1, bits(t2), bits(t1));
+        d = bits(t2 - t1);
         return bits(__builtin_elementwise_max(t1, t2));
     }
     static __device__ __forceinline__ uint32_t sub(uint32_t a, uint32_t b) { return bits(as(a) - as(b)); }
@@ -350,21 +405,28 @@ struct Pk<B16> {
 template <>
 struct Pk<F16> {
     typedef _Float16 v2 __attribute__((ext_vector_type(2)));
+    static constexpr bool kInvert = false;  // sign(t1 - t2) = take: own wins ties (__hlt2_mask is strict)
     static __device__ __forceinline__ uint32_t cvt(int a) { return (uint32_t)__builtin_bit_cast(uint16_t, (_Float16)a); }
     static __device__ __forceinline__ v2 as(uint32_t x) { return __builtin_bit_cast(v2, x); }
     static __device__ __forceinline__ uint32_t bits(v2 x) { return __builtin_bit_cast(uint32_t, x); }
-    // own predecessor wins ties (__hlt2_mask is strict, viterbiACS.cuh:147-157,250-256)
-    static __device__ __forceinline__ uint32_t acs(uint32_t own, uint32_t oth, uint32_t m, uint32_t& a0, uint32_t& a1)
+    // viterbiACS.cuh:147-157,250-256; metrics stay exact integers below 2048 in magnitude
+    static __device__ __forceinline__ uint32_t acs(uint32_t own, uint32_t oth, uint32_t m, uint32_t& d)
     {
         v2 t1 = as(own) + as(m), t2 = as(oth) - as(m);
-        a0 = dec_gt_f16lo(a0, bits(t2), bits(t1));
-        a1 = dec_gt_f16hi(a1, bits(t2), bits(t1));
+        d = bits(t1 - t2);
         return bits(__builtin_elementwise_max(t1, t2));
     }
     static __device__ __forceinline__ uint32_t sub(uint32_t a, uint32_t b) { return bits(as(a) - as(b)); }
 };
+// shift both halves right by one and insert the two sign bits of d at bits 15 and 31
+__device__ __forceinline__ uint32_t pk_push(uint32_t acc, uint32_t d)
+{
+    typedef unsigned short u2 __attribute__((ext_vector_type(2)));
+    uint32_t sh = __builtin_bit_cast(uint32_t, __builtin_bit_cast(u2, acc) >> (u2){1, 1});
+    return (d & 0x80008000u) | (sh & 0x7FFF7FFFu);
+}
 
-template <int CH, int CORE, int OB>
+template <int CH, int CORE, int OB, int ABL = 0>
 __global__ __launch_bounds__(64) void vd_decode_pk(const void* __restrict__ in, void* __restrict__ out, Geom geo)
 {
     using IN = In<CH>;
@@ -391,14 +453,14 @@ __global__ __launch_bounds__(64) void vd_decode_pk(const void* __restrict__ in, 
     const int bp_addr = (lane ^ 32) * 4;
     const uint32_t* tabu = (const uint32_t*)tab;
 
-    uint32_t pm = 0, acc0 = 0, acc1 = 0;
+    uint32_t pm = 0, acc = 0, accLo = 0;
     uint32_t kb = 0;
     typename IN::raw_t raw = IN::load(in, start + (uint64_t)li, avail);
 
     for (uint32_t j = 0; j < nblk; j++) {
         {
             int A, B;
-            IN::ab(raw, start + 32ull * j + li, A, B);
+            IN::ab(raw, start + 32ull * j + li, avail, A, B);
             uint32_t a = P::cvt(A), b = P::cvt(B), na = P::cvt(-A), nb = P::cvt(-B);
             uint32_t pa = __shfl_xor(a, 32), pb = __shfl_xor(b, 32), pna = __shfl_xor(na, 32), pnb = __shfl_xor(nb, 32);
             if (half == 0)
@@ -413,9 +475,12 @@ __global__ __launch_bounds__(64) void vd_decode_pk(const void* __restrict__ in, 
                 constexpr int i = decltype(I)::value;
                 constexpr int K = (PH + i) % 6;
                 constexpr int Q = (K + 5) % 6;
-                const uint32_t m = tabu[i * 4 + (L4[K] >> 2)];
-                const uint32_t oth = (uint32_t)xchg<Q>((int)pm, bp_addr);
-                pm = P::acs(pm, oth, m, acc0, acc1);
+                const uint32_t m = (ABL & 4) ? (uint32_t)L4[K] : tabu[i * 4 + (L4[K] >> 2)];
+                const uint32_t oth = (uint32_t)xchg<Q, ABL>((int)pm, bp_addr);
+                uint32_t d;
+                pm = P::acs(pm, oth, m, d);
+                if constexpr (!(ABL & 8)) acc = pk_push(acc, d);
+                if constexpr (i == 15) accLo = acc;  // first half-block complete
             });
         };
         switch (j % 3) {
@@ -427,16 +492,16 @@ __global__ __launch_bounds__(64) void vd_decode_pk(const void* __restrict__ in, 
         pm = P::sub(pm, __builtin_amdgcn_readfirstlane(pm));
         __syncthreads();
         if (j >= 1) {
-            ring[(j - 1 - kb) * 128 + lane] = acc0;
-            ring[(j - 1 - kb) * 128 + 64 + lane] = acc1;
+            ring[(j - 1 - kb) * 128 + lane] = P::kInvert ? ~accLo : accLo;
+            ring[(j - 1 - kb) * 128 + 64 + lane] = P::kInvert ? ~acc : acc;
         }
         if (j >= 2 && (j - 1 - kb == (uint32_t)kTB || j == nblk - 1)) {
             __syncthreads();
             const uint32_t hi = (j - 1) < Smy ? (j - 1) : Smy;  // words kb .. min(j-1,S)-1 of my chunk
             const uint32_t nw = hi > kb ? hi - kb : 0;
-            if ((uint32_t)li < nw) {
+            if (!(ABL & 1) && (uint32_t)li < nw) {
                 const uint64_t k = kb + li;
-                uint32_t w = traceback_word((const char*)ring, 512, half * 256, li, k);
+                uint32_t w = traceback_word<true>((const char*)ring, half, li, k);
                 if constexpr (OB == 32) {
                     ((uint32_t*)out)[my.startWord + k] = w;
                 } else {
@@ -446,8 +511,8 @@ __global__ __launch_bounds__(64) void vd_decode_pk(const void* __restrict__ in, 
                 }
             }
             __syncthreads();
-            ring[lane] = acc0;
-            ring[64 + lane] = acc1;
+            ring[lane] = P::kInvert ? ~accLo : accLo;
+            ring[64 + lane] = P::kInvert ? ~acc : acc;
             kb = j - 1;
         }
     }

@@ -1,0 +1,89 @@
+"""CPU tests of the product boundary: the C-ABI library loads, exports every symbol include/vd_capi.h
+declares, and its host-side logic (option filter, size helpers, reference harness, BER count)
+agrees with the oracle.  No decode is run here (no GPU in this container)."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HDR = os.path.join(ROOT, "include", "vd_capi.h")
+
+ALL_OPTIONS = [i | m | o | c for i in range(5) for m in (0x00, 0x10, 0x20) for o in (0x000, 0x100)
+               for c in (0x0000, 0x1000)]
+
+
+def header_functions():
+    src = open(HDR).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(vd_[a-z_]+)\s*\(", src)))
+
+
+def test_library_exports_every_header_symbol(vd):
+    names = header_functions()
+    assert len(names) >= 16
+    lib = ctypes.CDLL(vd.LIB_PATH)
+    for n in names:
+        assert hasattr(lib, n), f"{n} declared in include/vd_capi.h but not exported"
+    assert sorted(vd.EXPORTS) == names
+
+
+def test_options_valid_matches_reference_filter(vd, vo):
+    for o in ALL_OPTIONS:
+        assert vd.options_valid(o) == vo.options_valid(o), hex(o)
+    assert sum(vd.options_valid(o) for o in ALL_OPTIONS) == 42
+    assert not vd.options_valid(0x10000)
+
+
+@pytest.mark.parametrize("n", [128, 130, 1000, 2_000_000, 64_000_000, 512_000_000])
+def test_size_helpers_match_oracle(vd, vo, n):
+    for o in ALL_OPTIONS:
+        if not vd.options_valid(o):
+            continue
+        L = vd.lib()
+        assert L.vd_input_size(o, n) == vo.input_size(o, n)
+        assert L.vd_message_len(o, n) == vo.message_len(o, n)
+        assert L.vd_output_size(o, n) == vo.output_size(o, n)
+
+
+def test_reference_cli_sizes(vd):
+    d = vd.ViterbiCUDA.__new__(vd.ViterbiCUDA)  # size helpers only, no device object
+    d.options = vd.SOFT8 | vd.M_B16
+    assert d.getMessageLen(64_000_000) == 31_999_936
+    assert d.getOutputSize(64_000_000) == 3_999_992
+    assert d.getInputSize(64_000_000) == 64_000_000
+    assert vd.lib().vd_num_chunks() == 6400
+
+
+@pytest.mark.parametrize("opt", [0x0, 0x1, 0x2, 0x3, 0x4, 0x2 | 0x10])
+def test_host_harness_matches_oracle_restatement(vd, vo, opt):
+    # product harness (std:: generators) == oracle restatement (explicit mt19937 + polar method)
+    bits_a, packed_a = vd.simulate_host(opt, 40_000, 1.3, 5, 6)
+    bits_b, packed_b = vo.simulate(opt, 40_000, 1.3, 5, 6)
+    assert np.array_equal(bits_a, bits_b)
+    assert packed_a.tobytes() == packed_b.tobytes()
+
+
+def test_count_errors_matches_oracle(vd, vo):
+    opt = vo.HARD | vo.M_B32
+    bits, packed = vo.simulate(opt, 200_000, 0.5, 3, 4)
+    dec, _ = vo.decode(opt, packed)
+    assert vd.count_errors(opt, bits, dec) == vo.ben(opt, bits, dec)
+    opt16 = opt | vo.O_B16
+    dec16, _ = vo.decode(opt16, packed)
+    assert vd.count_errors(opt16, bits, dec16) == vo.ben(opt16, bits, dec16)
+
+
+def test_invalid_options_raise(vd):
+    with pytest.raises(vd.VitdecError):
+        vd.ViterbiCUDA(vd.SOFT8 | vd.M_FP16)
+
+
+def test_no_device_fails_loudly(vd):
+    # no GPU here: creating a decoder must raise, never fall back to a CPU path
+    if vd.device_count() > 0:
+        pytest.skip("GPU visible")
+    with pytest.raises(vd.VitdecError):
+        vd.ViterbiCUDA(vd.HARD | vd.M_B32)
