@@ -35,7 +35,8 @@ enum Ch : int { HARD = 0, SOFT4 = 1, SOFT8 = 2, SOFT16 = 3, FP32 = 4 };
 enum Core : int { B32 = 0, B16 = 1, F16 = 2 };
 
 constexpr int kChunks = 6400;  // reference blocksNum_total = 16*400 (viterbi.cu:19)
-constexpr int kTB = 16;        // output words traced back per batch
+constexpr int kTB = 16;        // output words traced back per batch (packed kernel)
+constexpr int kTBsc = 14;      // fp32 kernel: 14 words per batch keeps 7 four-wave workgroups per CU
 
 struct Geom {
     uint64_t packNum;      // output words of bpp bits (getMessageLen / bpp)
@@ -239,6 +240,58 @@ __device__ __forceinline__ uint32_t traceback_word(const char* ring, int h, int 
     return word;
 }
 
+// ---------------------------------------------------------------- traceback, fp32 kernel ring format
+// ring: per block slot 64 words (lane p), bit 31-s = take-bit of stage s.  `Q` is a byte offset from
+// the (256-B aligned) ring array holding base + 4p, so a step is one ds_read at Q and one bitop3
+// (Q ^= d & MK), and the ds_read address needs no add.  The decoded bits are not extracted per step:
+// with b_t = bit q_t of p_{t-1} and p's bit q_t untouched between stages t+5 and t, b_t = b_{t+6} ^ d_t,
+// so the word is the stride-6 prefix XOR of the collected decision bits D, seeded by the six bits
+// of the position reached at the end of the convergence phase.
+__device__ __forceinline__ uint32_t bitop3_xor_and(uint32_t a, uint32_t b, uint32_t c)
+{
+    return a ^ (b & c);  // v_bitop3_b32
+}
+__device__ __forceinline__ uint32_t traceback_word_sc(const char* ringb, uint32_t Q, uint64_t k)
+{
+    const int e6 = (int)((95 + 32 * k) % 6);  // stage phase of the traceback start
+    uint32_t MK[6];
+    sfor<6>([&](auto R) {
+        constexpr int r = decltype(R)::value;
+        int q = ((e6 - r + 6) % 6 + 5) % 6;
+        MK[r] = 4u << q;
+    });
+    // convergence: block k+2, stages 95+32k .. 64+32k
+    sfor<32>([&](auto I) {
+        constexpr int i = decltype(I)::value;
+        uint32_t w = *(const uint32_t*)(ringb + Q);
+        uint32_t d = (uint32_t)((int)(w << (31 - i)) >> 31);  // bit i = stage 31-i of the block
+        Q = bitop3_xor_and(Q, d, MK[i % 6]);
+    });
+    const uint32_t p = (Q >> 2) & 63u;  // position at stage 63+32k
+    Q -= 256u;
+    // emit: block k+1, stages 63+32k .. 32+32k; D bit j = take-bit at stage 63+32k-j
+    uint32_t D = 0;
+    sfor<32>([&](auto J) {
+        constexpr int j = decltype(J)::value;
+        uint32_t w = *(const uint32_t*)(ringb + Q);
+        D = (D & ~(1u << j)) | (w & (1u << j));
+        if constexpr (j < 31) {
+            uint32_t d = (uint32_t)((int)(w << (31 - j)) >> 31);
+            Q = bitop3_xor_and(Q, d, MK[(j + 32) % 6]);
+        }
+    });
+    // seed: E_j = bit q(63+32k-j) of p for j < 6 = brev6(rotr6(p, (q0+1) % 6)), q0 = q(63+32k)
+    const int q0 = ((e6 - 32 % 6 + 6) % 6 + 5) % 6;
+    const int s = (q0 + 1) % 6;
+    const uint32_t y = ((p >> s) | (p << (6 - s))) & 63u;
+    const uint32_t E = __builtin_bitreverse32(y) >> 26;
+    uint32_t X = D ^ E;
+    X ^= X << 6;
+    X ^= X << 12;
+    X ^= X << 24;
+    return X;  // word bit i <-> stage 63+32k-i
+}
+
 // ================================================================ fp32 core: one chunk per wave
 // Every metric core (M_B32, M_B16, M_FP16) runs here in exact-integer fp32: branch metrics are
 // integers of magnitude <= 65534, path metrics stay below 2^22 after the per-block renormalisation,
@@ -279,8 +332,9 @@ template <int CH, int CORE, int OB, int ABL = 0>
 __global__ __launch_bounds__(64 * kWaves) void vd_decode_sc(const void* __restrict__ in, void* __restrict__ out, Geom geo)
 {
     using IN = In<CH>;
+    constexpr int TBS = kTBsc;
     __shared__ float4 tab_all[kWaves][96];                   // per stage of a 3-block group: BM[0..3]
-    __shared__ uint32_t ring_all[kWaves][(kTB + 1) * 64];    // per block: 64 words, bit 31-s = stage s
+    __shared__ __attribute__((aligned(256))) uint32_t ring_all[kWaves][(TBS + 1) * 64];  // bit 31-s = stage s
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     float4* tab = tab_all[wv];
@@ -305,6 +359,9 @@ __global__ __launch_bounds__(64 * kWaves) void vd_decode_sc(const void* __restri
 
     float pm = 0.0f;
     uint32_t kb = 0;
+    // first traceback batch is shortened per workgroup so the waves sharing a SIMD do not all enter
+    // their latency-bound traceback in the same block
+    uint32_t tbn = TBS - 3 * (blockIdx.x & 3);
     // Input of a 3-block group is loaded one group ahead (~96 stages of compute, several loaded-HBM
     // round trips) and turned into the group's branch-metric table at the head of the group.
     typename IN::raw_t rA = IN::load(in, start + li, avail);
@@ -339,12 +396,13 @@ __global__ __launch_bounds__(64 * kWaves) void vd_decode_sc(const void* __restri
         if (Tie<CORE>::kInvert) word = ~word;  // ring holds take-bits
         wave_sync();
         if (j >= 1) ring[(j - 1 - kb) * 64 + lane] = word;
-        if (j >= 2 && (j - 1 - kb == (uint32_t)kTB || j == nblk - 1)) {
+        if (j >= 2 && (j - 1 - kb == tbn || j == nblk - 1)) {
             wave_sync();
             const uint32_t nw = j - 1 - kb;  // words kb .. j-2
             if (!(ABL & 1) && (uint32_t)lane < nw) {
                 const uint64_t k = kb + lane;
-                uint32_t w = traceback_word<false>((const char*)ring, 0, lane, k);
+                const uint32_t Q0 = (uint32_t)(wv * (TBS + 1) * 256 + (lane + 1) * 256);
+                uint32_t w = traceback_word_sc((const char*)ring_all, Q0, k);
                 if constexpr (OB == 32) {
                     ((uint32_t*)out)[cr.startWord + k] = w;
                 } else {
@@ -356,6 +414,7 @@ __global__ __launch_bounds__(64 * kWaves) void vd_decode_sc(const void* __restri
             wave_sync();
             ring[lane] = word;  // block j becomes slot 0 of the next batch
             kb = j - 1;
+            tbn = TBS;
         }
         return j + 1 < nblk;
     };
