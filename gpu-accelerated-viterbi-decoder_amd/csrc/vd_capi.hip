@@ -161,6 +161,28 @@ static int ensure_capacity(vd_decoder* d, size_t inBytes, size_t outBytes)
     return VD_OK;
 }
 
+// Per-device progress board of the decode kernels' fairness controller (vd_kernels.h, Geom::fair).
+// Allocated and zeroed once per device, shared by every decoder and stream on it: the kernels
+// leave it at zero, and concurrent launches sharing it only perturb issue priorities.
+static unsigned long long* fair_board(int device)
+{
+    static std::mutex mu;
+    static std::vector<unsigned long long*> boards;
+    std::lock_guard<std::mutex> lk(mu);
+    if ((int)boards.size() <= device) boards.resize(device + 1, nullptr);
+    if (!boards[device]) {
+        void* p = nullptr;
+        if (hipMalloc(&p, vd::kFairSlots * sizeof(unsigned long long)) != hipSuccess) return nullptr;
+        if (hipMemset(p, 0, vd::kFairSlots * sizeof(unsigned long long)) != hipSuccess ||
+            hipDeviceSynchronize() != hipSuccess) {
+            (void)hipFree(p);
+            return nullptr;
+        }
+        boards[device] = (unsigned long long*)p;
+    }
+    return boards[device];
+}
+
 static int launch_decode(int options, const void* in_d, void* out_d, size_t inputNum, hipStream_t s)
 {
     launch_fn f = pick(options);
@@ -171,6 +193,10 @@ static int launch_decode(int options, const void* in_d, void* out_d, size_t inpu
     g.availStages = avail_stages(options, inputNum);
     g.nchunks = vd::kChunks;
     if (g.packNum == 0) return VD_OK;
+    int dev = 0;
+    VD_HIP(hipGetDevice(&dev));
+    g.fair = fair_board(dev);
+    if (!g.fair) return fail(VD_ERR_NOMEM, "progress board allocation failed");
     f(in_d, out_d, g, s);
     VD_HIP(hipGetLastError());
     return VD_OK;

@@ -42,7 +42,11 @@ struct Geom {
     uint64_t packNum;      // output words of bpp bits (getMessageLen / bpp)
     uint64_t availStages;  // stages readable from the input buffer
     uint32_t nchunks;
+    unsigned long long* fair;  // per-SIMD progress board (kFairSlots words, zero at rest) or null
 };
+// progress board: one 64-bit word per SIMD slot, (waves << 32) + blocks started; indexed by
+// (XCC, SE, SH, CU, SIMD) from the hardware wave id.  Only issue priority depends on it.
+constexpr int kFairSlots = 8 * 8 * 2 * 16 * 4;
 
 // ---------------------------------------------------------------- compile-time loop helper
 template <typename F, int... I>
@@ -310,6 +314,74 @@ template <> struct Tie<F16> { static constexpr bool kInvert = false; };
 
 __device__ __forceinline__ float clamp01(float x) { return __builtin_amdgcn_fmed3f(x, 0.0f, 1.0f); }
 
+// ---------------------------------------------------------------- port-aware ACS stage (inline asm)
+// gfx950 VALU issue model (tools/vd_ubench2/3): a wave64 op starts every 2 cycles on one of two
+// ports and holds it for 4; add/sub/fma/fmac/cndmask/bitop3 may use either port, v_max only one,
+// and DPP / VOP3P ops hold both.  The compiler's order (add, sub_dpp, max, sub, fmac) serialises
+// at ~20 cycles a stage; this order keeps the DPP op alone and pairs max with the clamp-sub and the
+// previous stage's fmac with this stage's add: ~12 cycles.  Registers: pm metric, m own branch
+// metric, acc/bit decision accumulator (the fmac of stage t-1 runs in stage t), t1/t2 scratch.
+// DPP issue: an s_nop 0 right before each DPP op is worth ~7 cycles a stage (tools/vd_ubench6:
+// add,sub_dpp 21.1 -> add,s_nop,sub_dpp 14.1 cycles at 7 waves/SIMD); without it the DPP op stalls
+// the SIMD.  The DPP source (previous max) is >= 2 VALU ops back, as the data hazard requires.
+#define VD_DPP_CTRL_0 "quad_perm:[1,0,3,2]"
+#define VD_DPP_CTRL_1 "quad_perm:[2,3,0,1]"
+#define VD_DPP_CTRL_3 "row_ror:8"
+template <int Q, bool OWN_WINS>
+__device__ __forceinline__ void stage_dpp(float& pm, float& acc, float& bit, float m)
+{
+    float t1, t2;
+    if constexpr (Q == 2) {
+        float x;
+        // x = pm[lane ^ 7 within 8]; t2 = x[lane ^ 3 within 4] - m  ==  pm[lane ^ 4] - m
+        if constexpr (OWN_WINS)
+            asm("v_fma_f32 %0, %0, 2.0, %1\n\ts_nop 0\n\tv_mov_b32_dpp %5, %2 row_half_mirror row_mask:0xf bank_mask:0xf\n\t"
+                "v_add_f32 %3, %2, %6\n\ts_nop 0\n\tv_sub_f32_dpp %4, %5, %6 quad_perm:[3,2,1,0] row_mask:0xf bank_mask:0xf\n\t"
+                "v_max_f32 %2, %3, %4\n\tv_sub_f32_e64 %1, %4, %3 clamp"
+                : "+v"(acc), "+v"(bit), "+v"(pm), "=&v"(t1), "=&v"(t2), "=&v"(x) : "v"(m));
+        else
+            asm("v_fma_f32 %0, %0, 2.0, %1\n\ts_nop 0\n\tv_mov_b32_dpp %5, %2 row_half_mirror row_mask:0xf bank_mask:0xf\n\t"
+                "v_add_f32 %3, %2, %6\n\ts_nop 0\n\tv_sub_f32_dpp %4, %5, %6 quad_perm:[3,2,1,0] row_mask:0xf bank_mask:0xf\n\t"
+                "v_max_f32 %2, %3, %4\n\tv_sub_f32_e64 %1, %3, %4 clamp"
+                : "+v"(acc), "+v"(bit), "+v"(pm), "=&v"(t1), "=&v"(t2), "=&v"(x) : "v"(m));
+    } else {
+#define VD_STAGE_DPP(CTRL, CL)                                                                                  \
+    asm("v_fma_f32 %0, %0, 2.0, %1\n\tv_add_f32 %3, %2, %5\n\ts_nop 0\n\tv_sub_f32_dpp %4, %2, %5 " CTRL " row_mask:0xf bank_mask:0xf\n\t" \
+        "v_max_f32 %2, %3, %4\n\t" CL                                                                            \
+        : "+v"(acc), "+v"(bit), "+v"(pm), "=&v"(t1), "=&v"(t2) : "v"(m))
+        if constexpr (OWN_WINS) {
+            if constexpr (Q == 0) VD_STAGE_DPP(VD_DPP_CTRL_0, "v_sub_f32_e64 %1, %4, %3 clamp");
+            else if constexpr (Q == 1) VD_STAGE_DPP(VD_DPP_CTRL_1, "v_sub_f32_e64 %1, %4, %3 clamp");
+            else VD_STAGE_DPP(VD_DPP_CTRL_3, "v_sub_f32_e64 %1, %4, %3 clamp");
+        } else {
+            if constexpr (Q == 0) VD_STAGE_DPP(VD_DPP_CTRL_0, "v_sub_f32_e64 %1, %3, %4 clamp");
+            else if constexpr (Q == 1) VD_STAGE_DPP(VD_DPP_CTRL_1, "v_sub_f32_e64 %1, %3, %4 clamp");
+            else VD_STAGE_DPP(VD_DPP_CTRL_3, "v_sub_f32_e64 %1, %3, %4 clamp");
+        }
+#undef VD_STAGE_DPP
+    }
+}
+// exchanged metric already fetched (LDS permute); E: bit = clamp(t1 + e - t2) (M_B32 own-wins lanes)
+template <bool OWN_WINS, bool EBIAS>
+__device__ __forceinline__ void stage_lds(float& pm, float& acc, float& bit, float m, float oth, float e)
+{
+    float t1, t2;
+    if constexpr (EBIAS) {
+        float t1e;
+        asm("v_fma_f32 %0, %0, 2.0, %1\n\tv_add_f32 %3, %2, %6\n\tv_sub_f32 %4, %7, %6\n\tv_add_f32 %5, %3, %8\n\t"
+            "v_max_f32 %2, %3, %4\n\tv_sub_f32_e64 %1, %5, %4 clamp"
+            : "+v"(acc), "+v"(bit), "+v"(pm), "=&v"(t1), "=&v"(t2), "=&v"(t1e) : "v"(m), "v"(oth), "v"(e));
+    } else if constexpr (OWN_WINS) {
+        asm("v_fma_f32 %0, %0, 2.0, %1\n\tv_add_f32 %3, %2, %5\n\tv_sub_f32 %4, %6, %5\n\t"
+            "v_max_f32 %2, %3, %4\n\tv_sub_f32_e64 %1, %4, %3 clamp"
+            : "+v"(acc), "+v"(bit), "+v"(pm), "=&v"(t1), "=&v"(t2) : "v"(m), "v"(oth));
+    } else {
+        asm("v_fma_f32 %0, %0, 2.0, %1\n\tv_add_f32 %3, %2, %5\n\tv_sub_f32 %4, %6, %5\n\t"
+            "v_max_f32 %2, %3, %4\n\tv_sub_f32_e64 %1, %3, %4 clamp"
+            : "+v"(acc), "+v"(bit), "+v"(pm), "=&v"(t1), "=&v"(t2) : "v"(m), "v"(oth));
+    }
+}
+
 template <int Q, int ABL = 0>
 __device__ __forceinline__ float xchgf(float x, int bp_addr)
 {
@@ -328,6 +400,12 @@ __device__ __forceinline__ void wave_sync()
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+__device__ __forceinline__ uint32_t simd_slot()
+{
+    const uint32_t h = __builtin_amdgcn_s_getreg(4 | (0 << 6) | (31 << 11));         // HW_ID
+    const uint32_t x = __builtin_amdgcn_s_getreg(20 | (0 << 6) | (31 << 11)) & 7u;  // XCC_ID
+    return (((x * 8 + ((h >> 13) & 7u)) * 2 + ((h >> 12) & 1u)) * 16 + ((h >> 8) & 15u)) * 4 + ((h >> 4) & 3u);
+}
 template <int CH, int CORE, int OB, int ABL = 0>
 __global__ __launch_bounds__(64 * kWaves) void vd_decode_sc(const void* __restrict__ in, void* __restrict__ out, Geom geo)
 {
@@ -341,6 +419,9 @@ __global__ __launch_bounds__(64 * kWaves) void vd_decode_sc(const void* __restri
     uint32_t* ring = ring_all[wv];
     const ChunkRange cr = chunk_range(geo, blockIdx.x * kWaves + wv);
     if (cr.words == 0) return;
+    // ABL & 32 (tools only): per-wave clock stamps at out + 16 MiB
+    const uint64_t t_clk0 = (ABL & 32) ? __builtin_amdgcn_s_memtime() : 0;
+    const uint64_t t_rt0 = (ABL & 32) ? __builtin_amdgcn_s_memrealtime() : 0;
     const uint64_t start = cr.startWord * OB;                      // first stage of the chunk
     const uint32_t S = OB == 32 ? cr.words : (cr.words + 1) / 2;  // 32-bit words traced back
     const uint32_t nblk = S + 2;                                   // 64 warm-up stages + S slides
@@ -359,6 +440,19 @@ __global__ __launch_bounds__(64 * kWaves) void vd_decode_sc(const void* __restri
 
     float pm = 0.0f;
     uint32_t kb = 0;
+    // Fairness: the SIMD arbiter favours the oldest wave, so left alone the waves sharing a SIMD
+    // finish up to 2x apart and the tail runs at low occupancy (tools/vd_ablate clock stamps).
+    // Each wave posts its progress to the SIMD's board word at every 3-block group and sets its
+    // issue priority from its lag behind the SIMD mean (ABL & 256 disables).
+    unsigned long long* fb = nullptr;
+    unsigned long long fret = 0;
+    uint32_t fadded = 0;
+    if constexpr (!(ABL & 256)) {
+        if (geo.fair) {
+            fb = geo.fair + simd_slot();
+            if (lane == 0) atomicAdd(fb, 1ull << 32);
+        }
+    }
     // first traceback batch is shortened per workgroup so the waves sharing a SIMD do not all enter
     // their latency-bound traceback in the same block
     uint32_t tbn = TBS - 3 * (blockIdx.x & 3);
@@ -372,25 +466,30 @@ __global__ __launch_bounds__(64 * kWaves) void vd_decode_sc(const void* __restri
     auto block = [&](auto PHc, uint32_t j) {
         constexpr int PH = decltype(PHc)::value;
         constexpr int TB0 = PH / 2;
-        float acc = 0.0f;
+        // decision bits: the fmac of stage t runs inside stage t+1 (see stage_dpp); acc restarts
+        // at each 16-stage half so its value stays an exact integer below 2^16
+        float acc = 0.0f, bit = 0.0f;
         uint32_t hi16 = 0, word = 0;
         sfor<32>([&](auto I) {
             constexpr int i = decltype(I)::value;
             constexpr int K = (PH + i) % 6;
             constexpr int Q = (K + 5) % 6;
             const float m = (ABL & 4) ? (float)L4[K] : tabf[(TB0 * 32 + i) * 4 + (L4[K] >> 2)];
-            const float oth = xchgf<Q, ABL>(pm, bp_addr);
-            const float t1 = pm + m, t2 = oth - m;
-            pm = fmaxf(t1, t2);  // the survivor value does not depend on the tie rule
-            float bit;
-            if constexpr (!Tie<CORE>::kInvert) bit = clamp01(t2 - t1);
-            else if constexpr (CORE == B32 && K == 0) bit = clamp01((t1 + ebias) - t2);
-            else bit = clamp01(t1 - t2);
-            if constexpr (ABL & 8) asm volatile("" ::"v"(bit));
-            else acc = (i == 0 || i == 16) ? bit : __builtin_fmaf(acc, 2.0f, bit);  // 16 bits per half
-            if constexpr (i == 15) hi16 = (uint32_t)acc;
-            if constexpr (i == 31) word = (hi16 << 16) | (uint32_t)acc;
+            constexpr bool OWN = !Tie<CORE>::kInvert;
+            if constexpr (Q <= 3 || (ABL & 2)) {
+                stage_dpp<(Q <= 3 ? Q : 3), OWN>(pm, acc, bit, m);
+            } else {
+                const float oth = xchgf<Q>(pm, bp_addr);
+                stage_lds<OWN, CORE == B32 && K == 0>(pm, acc, bit, m, oth, ebias);
+            }
+            if constexpr (i == 16) {  // acc now holds stages 0..15
+                hi16 = (uint32_t)acc;
+                acc = 0.0f;
+            }
         });
+        acc = __builtin_fmaf(acc, 2.0f, bit);  // stage 31's accumulate
+        word = (hi16 << 16) | (uint32_t)acc;
+        if constexpr (ABL & 8) asm volatile("" ::"v"(word));
         // decision-neutral renormalisation by the metric of position 0 (keeps |pm| < 2^22)
         pm -= __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, pm)));
         if (Tie<CORE>::kInvert) word = ~word;  // ring holds take-bits
@@ -419,6 +518,23 @@ __global__ __launch_bounds__(64 * kWaves) void vd_decode_sc(const void* __restri
         return j + 1 < nblk;
     };
     for (uint32_t j = 0;; j += 3) {
+        if constexpr (!(ABL & 256)) {
+            if (fb) {
+                if (j > 0) {
+                    // board value returned at the previous group head (own add of 3 not included)
+                    const uint64_t r = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(fret >> 32)) << 32) |
+                                       (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)fret);
+                    const int64_t n = (int64_t)(r >> 32), sum = (int64_t)(uint32_t)r + 3;
+                    const int64_t d = (int64_t)j * n - sum;  // (own - mean) * n, in blocks
+                    if (d <= -3 * n) __builtin_amdgcn_s_setprio(3);
+                    else if (d <= 0) __builtin_amdgcn_s_setprio(2);
+                    else if (d <= 3 * n) __builtin_amdgcn_s_setprio(1);
+                    else __builtin_amdgcn_s_setprio(0);
+                }
+                if (lane == 0) fret = atomicAdd(fb, 3ull);
+                fadded += 3;
+            }
+        }
         if (lane < 32) {
             int A, B;
             IN::ab(rA, start + 32ull * j + li, avail, A, B);
@@ -440,6 +556,18 @@ __global__ __launch_bounds__(64 * kWaves) void vd_decode_sc(const void* __restri
         wave_sync();  // this group's table reads complete before the next group overwrites it
     }
     if constexpr (ABL & 8) asm volatile("" ::"v"(pm));
+    if constexpr (!(ABL & 256)) {
+        if (fb && lane == 0) atomicAdd(fb, 0ull - ((1ull << 32) + fadded));  // board back to zero
+    }
+    if constexpr (ABL & 32) {
+        const uint64_t c1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+        if (lane == 0) {
+            uint64_t* d = (uint64_t*)((char*)out + (16u << 20)) + 6 * (blockIdx.x * kWaves + wv);
+            d[0] = t_clk0; d[1] = c1; d[2] = t_rt0; d[3] = r1;
+            d[4] = (uint32_t)__builtin_amdgcn_s_getreg(4 | (0 << 6) | (31 << 11));   // HW_ID
+            d[5] = (uint32_t)__builtin_amdgcn_s_getreg(20 | (0 << 6) | (31 << 11));  // XCC_ID
+        }
+    }
 }
 
 // ================================================================ packed cores: two chunks per wave

@@ -23,7 +23,7 @@ int main(int argc, char** argv)
     const size_t inBytes = inputNum;  // SOFT8 (largest of the two)
     void *in, *out;
     CK(hipMalloc(&in, inBytes));
-    CK(hipMalloc(&out, N / 8 + 64));
+    CK(hipMalloc(&out, (16u << 20) + 6400 * 48));
     std::vector<uint32_t> h(inBytes / 4);
     uint32_t x = 12345;
     for (auto& w : h) { x ^= x << 13; x ^= x >> 17; x ^= x << 5; w = x; }
@@ -32,10 +32,12 @@ int main(int argc, char** argv)
     g.packNum = (N - 64) / 32;
     g.nchunks = 6400;
     g.availStages = N;
+    CK(hipMalloc(&g.fair, vd::kFairSlots * 8));
+    CK(hipMemset(g.fair, 0, vd::kFairSlots * 8));
     std::vector<Var> v;
     addb<0>(v, "sc hard/b32 full"); addb<1>(v, "sc hard/b32 -traceback"); addb<2>(v, "sc hard/b32 lds-xchg->dpp");
     addb<4>(v, "sc hard/b32 -bmread"); addb<8>(v, "sc hard/b32 -decisions"); addb<15>(v, "sc hard/b32 skeleton");
-    addb<16>(v, "sc hard/b32 -loads"); addb<17>(v, "sc hard/b32 -loads-traceback"); addb<31>(v, "sc hard/b32 skel-loads");
+    addb<16>(v, "sc hard/b32 -loads"); addb<17>(v, "sc hard/b32 -loads-traceback"); addb<31>(v, "sc hard/b32 skel-loads"); addb<256>(v, "sc hard/b32 -fairness"); adds<256>(v, "sc soft8/b16 -fairness");
     adds<0>(v, "sc soft8/b16 full"); adds<1>(v, "sc soft8/b16 -traceback"); adds<16>(v, "sc soft8/b16 -loads");
     addp<0>(v, "pk soft8/b16 full"); addp<1>(v, "pk soft8/b16 -traceback");
     hipEvent_t e0, e1;
@@ -55,6 +57,44 @@ int main(int argc, char** argv)
         std::sort(t[i].begin(), t[i].end());
         printf("%-26s median %.4f ms  min %.4f ms  -> %.1f Gb/s\n", v[i].name, t[i][t[i].size() / 2], t[i][0],
                (double)(N - 64) / (t[i][t[i].size() / 2] * 1e-3) / 1e9);
+    }
+    // per-wave clock stamps of the full kernel (ABL 32), without and with the priority schedule (64)
+    for (KFn f : {(KFn)vd::vd_decode_sc<vd::HARD, vd::B32, 32, 32>, (KFn)vd::vd_decode_sc<vd::HARD, vd::B32, 32, 288>}) {
+        printf("=== %s\n", f == (KFn)vd::vd_decode_sc<vd::HARD, vd::B32, 32, 32> ? "full" : "full -fairness");
+        for (int r = 0; r < 3; r++) hipLaunchKernelGGL(f, dim3(1600), dim3(256), 0, 0, in, out, g);
+        CK(hipDeviceSynchronize());
+        std::vector<uint64_t> d(6400 * 6);
+        CK(hipMemcpy(d.data(), (char*)out + (16u << 20), d.size() * 8, hipMemcpyDeviceToHost));
+        uint64_t c0 = ~0ull, r0 = ~0ull, r1 = 0; std::vector<double> cyc, mhz, startus, endus;
+        for (int w = 0; w < 6400; w++) { r0 = std::min(r0, d[6 * w + 2]); r1 = std::max(r1, d[6 * w + 3]); }
+        std::vector<int> per_simd(8 * 64 * 4 * 4 * 4, 0);
+        for (int w = 0; w < 6400; w++) {
+            const uint64_t* e = &d[6 * w];
+            cyc.push_back((double)(e[1] - e[0]));
+            mhz.push_back((double)(e[1] - e[0]) / (double)(e[3] - e[2]) * 100.0);
+            startus.push_back((e[2] - r0) / 100.0); endus.push_back((e[3] - r0) / 100.0);
+        }
+        auto pr = [](const char* n, std::vector<double> v) { std::sort(v.begin(), v.end());
+            printf("%-22s min %.1f  p10 %.1f  med %.1f  p90 %.1f  max %.1f\n", n, v[0], v[v.size() / 10], v[v.size() / 2], v[v.size() * 9 / 10], v.back()); };
+        printf("kernel span (realtime) %.1f us\n", (r1 - r0) / 100.0);
+        pr("wave cycles", cyc); pr("clock MHz", mhz); pr("wave start us", startus); pr("wave end us", endus);
+        printf("cycles/stage (median wave, 5088 stages): %.2f\n", [&]{ auto v = cyc; std::sort(v.begin(), v.end()); return v[v.size()/2] / 5088.0; }());
+        // waves per (xcc, se, cu, simd) from HW_ID: wave_id[3:0] simd_id[5:4] cu_id[11:8] sh_id[12] se_id[15:13]
+        std::vector<int> cnt(8 * 8 * 2 * 16 * 4, 0);
+        for (int w = 0; w < 6400; w++) {
+            uint32_t h = (uint32_t)d[6 * w + 4], x = (uint32_t)d[6 * w + 5] & 7;
+            int simd = (h >> 4) & 3, cu = (h >> 8) & 15, sh = (h >> 12) & 1, se = (h >> 13) & 7;
+            cnt[(((x * 8 + se) * 2 + sh) * 16 + cu) * 4 + simd]++;
+        }
+        std::vector<int> hist(16, 0); int used = 0;
+        for (int c : cnt) if (c) { used++; hist[std::min(c, 15)]++; }
+        std::vector<unsigned long long> fb(vd::kFairSlots);
+        CK(hipMemcpy(fb.data(), g.fair, fb.size() * 8, hipMemcpyDeviceToHost));
+        int nz = 0; for (auto x : fb) nz += x != 0;
+        printf("progress board words non-zero after run: %d\n", nz);
+        printf("SIMDs used %d; waves-per-SIMD histogram:", used);
+        for (int i = 0; i < 16; i++) if (hist[i]) printf(" %d:%d", i, hist[i]);
+        printf("\n");
     }
     return 0;
 }
