@@ -30,6 +30,7 @@ import vitdec  # noqa: E402
 N_BITS = 32_000_000
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md)
 SNR_DB = 2.0
+PMC_ROUND = "r01"  # profiles/<round>/pmc_summary.json
 
 WORKLOADS = [
     ("hard_b32", vitdec.HARD | vitdec.M_B32 | vitdec.O_B32),
@@ -42,28 +43,82 @@ def algorithmic_bytes(opt, input_num):
     return vitdec.lib().vd_input_size(opt, input_num) + vitdec.lib().vd_output_size(opt, input_num)
 
 
-def cpu_baseline(sample_bits=2_000_000):
-    """Scalar host Viterbi (the oracle's CPU restatement, 1 thread) on a bounded sample."""
+def cpu_baseline(batches):
+    """Scalar host Viterbi (the oracle's CPU restatement, 1 thread) on the bench's own inputs.
+
+    The sample is the full workload of one step: the same two 32M-bit batches the GPU decoded
+    (copied from HBM), same 6400-chunk partition.  Its output is also compared word-for-word with
+    the GPU output, so the bench line carries a full-size parity check."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import vd_oracle as vo
-    opt = WORKLOADS[0][1]
-    _, packed = vo.simulate(opt, sample_bits, SNR_DB, 1, 2)
-    t0 = time.perf_counter()
-    out, _ = vo.decode(opt, packed, nthreads=1)
-    dt = time.perf_counter() - t0
-    bits = vo.message_len(opt, 2 * sample_bits)
+    dt = 0.0
+    bits = 0
+    match = True
+    for b in batches:
+        packed = b["inp"].cpu().numpy().view(np.float32 if (b["opt"] & 0xF) == vitdec.FP32 else np.int32)
+        t0 = time.perf_counter()
+        out, _ = vo.decode(b["opt"], packed, input_num=b["input_num"], nthreads=1)
+        dt += time.perf_counter() - t0
+        bits += b["msg"]
+        gpu = b["out"].cpu().numpy().view(out.dtype)
+        match = match and bool(np.array_equal(out, gpu))
+    names = " + ".join(b["name"] for b in batches)
     return {"value": round(bits / dt / 1e9, 6), "unit": "Gb/s", "cores": 1, "kind": "port",
-            "sample": f"HARD int32-metric decode of a {sample_bits // 1_000_000}M-bit message (1/16 of the "
-                      f"32M batch, same 6400-chunk partition), oracle/vd_oracle.c on 1 host thread, {dt:.1f} s"}
+            "sample": f"one full bench step ({names}, 2 x 32M-bit batches, 6400-chunk partition) decoded by "
+                      f"oracle/vd_oracle.c on 1 host thread in {dt:.1f} s; output identical to the GPU's: {match}",
+            "matches_gpu": match}
 
 
-def load_traffic():
-    """HBM bytes per launch from the committed rocprofv3 PMC summary (profiles/), if present."""
-    p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+def load_pmc():
+    """Per-kernel PMC summary committed under profiles/ (tools/pmc_summary.py over rocprofv3 --pmc
+    passes of this bench): HBM bytes per launch (FETCH_SIZE x2 gfx950 correction + WRITE_SIZE) and
+    VALU instruction counts."""
+    p = os.path.join(ROOT, "profiles", PMC_ROUND, "pmc_summary.json")
     if os.path.exists(p):
         with open(p) as f:
             return json.load(f)
     return {}
+
+
+CLOCK_HZ = 2.4e9  # gfx950 peak engine clock (MI355X_MICROARCH.md)
+N_SIMD = 1024     # 256 CUs x 4 SIMDs
+
+
+def stages_per_launch(opt, input_num):
+    """wave-stages one decode launch runs: every chunk decodes its words plus a 64-stage window."""
+    bpp = 16 if (opt & 0xF00) == vitdec.O_B16 else 32
+    pack = vitdec.lib().vd_message_len(opt, input_num) // bpp
+    n = vitdec.lib().vd_num_chunks()
+    base, rem = divmod(pack, n)
+    total = 0
+    for words, cnt in ((base + 1, rem), (base, n - rem)):
+        if words:
+            total += cnt * (64 + (words * bpp + 31) // 32 * 32)
+    return total
+
+
+def rank_seed(rank, workload_index):
+    """Seed of the synthetic batch a rank decodes: independent batches per rank (weak scaling)."""
+    return 1000 * rank + workload_index + 1
+
+
+def aggregate_gbps(bits_per_step, world, steps, elapsed_s):
+    """Whole-job throughput: every rank decodes bits_per_step per step; elapsed is the max over ranks."""
+    return bits_per_step * world * steps / elapsed_s / 1e9
+
+
+def max_over_ranks(elapsed, dev):
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+    return float(t.item())
+
+
+def gather_checksums(sums, dev, world):
+    """The only cross-rank traffic: per-rank XOR checksums of the decoded words (after timing)."""
+    cs = torch.tensor(sums, dtype=torch.int64, device=dev)
+    gathered = [torch.empty_like(cs) for _ in range(world)]
+    torch.distributed.all_gather(gathered, cs)
+    return [[int(v) for v in g.cpu()] for g in gathered]
 
 
 def main():
@@ -95,7 +150,7 @@ def main():
         inp = torch.empty(nin, dtype=torch.uint8, device=dev)
         bits = torch.empty(N_BITS, dtype=torch.uint8, device=dev)
         out = torch.empty(nout, dtype=torch.uint8, device=dev)
-        vitdec.synth_device(opt, N_BITS, SNR_DB, 1000 * rank + wi + 1, bits.data_ptr(), inp.data_ptr(), sptr)
+        vitdec.synth_device(opt, N_BITS, SNR_DB, rank_seed(rank, wi), bits.data_ptr(), inp.data_ptr(), sptr)
         dec = vitdec.ViterbiCUDA(opt, 0, dev)
         batches.append(dict(name=name, opt=opt, input_num=input_num, inp=inp, out=out, bits=bits, dec=dec,
                             msg=vitdec.lib().vd_message_len(opt, input_num)))
@@ -139,23 +194,31 @@ def main():
         bers.append(vitdec.count_errors(b["opt"], bits_h, out_h) / b["msg"])
         sums.append(int(np.bitwise_xor.reduce(out_h.view(np.uint32))))
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-        elapsed = float(t.item())
-        cs = torch.tensor(sums, dtype=torch.int64, device=dev)
-        gathered = [torch.empty_like(cs) for _ in range(world)]
-        torch.distributed.all_gather(gathered, cs)
+        elapsed = max_over_ranks(elapsed, dev)
+        gathered = gather_checksums(sums, dev, world)
+    else:
+        gathered = [sums]
 
     if rank == 0:
         bits_per_step = sum(b["msg"] for b in batches)
         ms_per_step = elapsed / args.steps * 1e3
-        value = bits_per_step * world * args.steps / elapsed / 1e9
+        value = aggregate_gbps(bits_per_step, world, args.steps, elapsed)
         # dominant kernel roofline (HBM, algorithmic bytes = packed input + packed output)
         di = int(np.argmax(kms))
         db = batches[di]
         alg = algorithmic_bytes(db["opt"], db["input_num"])
         achieved = alg / (kms[di] * 1e-3) / 1e9
-        traffic = load_traffic().get(db["name"])
+        pmc = load_pmc().get(db["name"], {})
+        traffic = pmc.get("traffic_bytes")
+        # VALU issue view of the same kernel (the bound that actually binds)
+        stages = stages_per_launch(db["opt"], db["input_num"])
+        valu = None
+        if "valu_insts_per_wave" in pmc:
+            insts = pmc["valu_insts_per_wave"] * vitdec.lib().vd_num_chunks()
+            valu = {"insts_per_launch": round(insts), "insts_per_wave_stage": round(insts / stages, 3),
+                    "wave_stages_per_launch": stages,
+                    "issue_cycles_per_inst_per_simd": round(kms[di] * 1e-3 * CLOCK_HZ * N_SIMD / insts, 3),
+                    "source": f"profiles/{PMC_ROUND}/pmc_summary.json (SQ_INSTS_VALU)"}
         result = {
             "metric": "decoded Gb/s at K=7 R=1/2, 32M bits, hard+soft8",
             "value": round(value, 3),
@@ -191,10 +254,13 @@ def main():
                 "frac": round(achieved / HBM_PEAK_GBS, 5),
                 "traffic": traffic,
                 "algorithmic_bytes_per_launch": alg,
+                "traffic_source": f"profiles/{PMC_ROUND}/pmc_summary.json (FETCH_SIZE x2 + WRITE_SIZE)",
+                "valu": valu,
             },
+            "checksums": [[hex(x) for x in g] for g in gathered],
         }
         if not args.no_cpu_baseline and world == 1:
-            result["cpu_baseline"] = cpu_baseline()
+            result["cpu_baseline"] = cpu_baseline(batches)
         print(json.dumps(result), flush=True)
 
     for b in batches:

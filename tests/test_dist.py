@@ -1,0 +1,66 @@
+"""world_size-2 `gloo` tests (CPU) of bench.py's multi-GPU host logic.
+
+The decode path shards by independent batches: each rank synthesises and decodes its own batches,
+there is no collective on the data path, the step time is the max over ranks and the only
+cross-rank traffic is one all_gather of per-rank checksums after the timed region.  The same
+functions run under RCCL on the GPU box (bench.py under torch.distributed.run)."""
+import os
+import socket
+import sys
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    sys.path.insert(0, ROOT)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import bench
+    elapsed = 1.0 + rank  # rank 1 is the slow one
+    m = bench.max_over_ranks(elapsed, "cpu")
+    sums = [0xDEAD0000 + rank, 0xBEEF0000 + rank]  # uint32 checksums, as bench computes them
+    g = bench.gather_checksums(sums, "cpu", world)
+    seeds = [bench.rank_seed(rank, wi) for wi in range(2)]
+    q.put((rank, m, g, seeds))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_rank_gloo_sharding():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, m, g, seeds in res:
+        assert m == 2.0  # max over ranks
+        assert g == [[0xDEAD0000, 0xBEEF0000], [0xDEAD0001, 0xBEEF0001]]
+    all_seeds = [s for _, _, _, seeds in res for s in seeds]
+    assert len(set(all_seeds)) == len(all_seeds)  # every rank decodes independent batches
+
+
+def test_aggregate_is_whole_job():
+    sys.path.insert(0, ROOT)
+    import bench
+    # 2 ranks x 2 batches x 31,999,936 bits in 1 step of 1 ms -> 256 Gb/s whole-job
+    assert bench.aggregate_gbps(2 * 31_999_936, 2, 1, 1e-3) == pytest.approx(127.999744)
+    assert bench.stages_per_launch(0x0, 64_000_000) == 1598 * 5088 + 4802 * 5056
