@@ -17,6 +17,7 @@
 
 #include "../../include/vd_capi.h"
 #include "vd_kernels.h"
+#include "vd_kernel_tg.h"
 #include "vd_synth.h"
 
 namespace {
@@ -94,8 +95,13 @@ using launch_fn = void (*)(const void*, void*, vd::Geom, hipStream_t);
 template <int CH, int CORE, int OB>
 void launch_t(const void* in, void* out, vd::Geom g, hipStream_t s)
 {
-    hipLaunchKernelGGL((vd::vd_decode_sc<CH, CORE, OB>), dim3((g.nchunks + vd::kWaves - 1) / vd::kWaves),
-                       dim3(64 * vd::kWaves), 0, s, in, out, g);
+    // tagged-metric kernel everywhere but SOFT16 (whose metrics leave no room for the tags)
+    if constexpr (CH == vd::SOFT16)
+        hipLaunchKernelGGL((vd::vd_decode_sc<CH, CORE, OB>), dim3((g.nchunks + vd::kWaves - 1) / vd::kWaves),
+                           dim3(64 * vd::kWaves), 0, s, in, out, g);
+    else
+        hipLaunchKernelGGL((vd::vd_decode_tg<CH, CORE, OB>), dim3((g.nchunks + vd::kWaves - 1) / vd::kWaves),
+                           dim3(64 * vd::kWaves), 0, s, in, out, g);
 }
 
 template <int CH, int CORE>
@@ -120,11 +126,11 @@ launch_fn pick(int o)
 const char* kname(int o)
 {
     static const char* names[5][3] = {
-        {"vd_decode_sc<HARD,B32>", "vd_decode_sc<HARD,B16>", "vd_decode_sc<HARD,F16>"},
-        {"vd_decode_sc<SOFT4,B32>", "vd_decode_sc<SOFT4,B16>", "vd_decode_sc<SOFT4,F16>"},
-        {"vd_decode_sc<SOFT8,B32>", "vd_decode_sc<SOFT8,B16>", "-"},
+        {"vd_decode_tg<HARD,B32>", "vd_decode_tg<HARD,B16>", "vd_decode_tg<HARD,F16>"},
+        {"vd_decode_tg<SOFT4,B32>", "vd_decode_tg<SOFT4,B16>", "vd_decode_tg<SOFT4,F16>"},
+        {"vd_decode_tg<SOFT8,B32>", "vd_decode_tg<SOFT8,B16>", "-"},
         {"vd_decode_sc<SOFT16,B32>", "-", "-"},
-        {"vd_decode_sc<FP32,B32>", "vd_decode_sc<FP32,B16>", "vd_decode_sc<FP32,F16>"},
+        {"vd_decode_tg<FP32,B32>", "vd_decode_tg<FP32,B16>", "vd_decode_tg<FP32,F16>"},
     };
     if (!valid(o)) return "-";
     return names[ch_of(o)][met_of(o)];

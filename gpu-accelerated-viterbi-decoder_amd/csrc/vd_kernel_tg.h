@@ -1,0 +1,369 @@
+// vd_kernel_tg.h -- "tagged" decode kernel vd_decode_tg (gfx950): the survivor decision of every stage
+// rides in the low bits of the fp32 path metric, so one add-compare-select is three VALU ops
+// (add, DPP-fused sub, max) instead of five, and two of the six butterfly distances move from LDS
+// permutes to VALU permlane swaps.  Same decode semantics as vd_decode_sc (reference hot path
+// src/viterbi/viterbi.cu:144-207, viterbiACS.cuh:113-157,216-256, viterbiTB.cuh:4-21): bit-exact for
+// every valid option except SOFT16, whose branch metrics (|BM| up to 65534) leave no room for the tags.
+//
+// Metric word.  V = metric * 2^S + h, an exact integer in fp32 (|V| < 2^24).  At stage j of a J-stage
+// history field (S = J+1), the own candidate gets tag +c*2^j and the exchanged one -c*2^j, c = +1 where
+// the reference's tie rule lets the own predecessor win ties, -1 where the exchanged one does:
+//   t1 = V_own + (BM*2^S + c*2^j),  t2 = V_exch - (BM*2^S + c*2^j),  V' = max(t1, t2).
+// The history h = sum of the chosen signed digits (+-2^i, i < j) satisfies |h| < 2^j, so on equal
+// metrics the tag decides (the tie rule), and on unequal metrics (a difference of >= 2^S) neither tags
+// nor history can flip the order: every decision equals the reference's int32/int16/fp16 decision.
+// After J stages the field is read out -- r = round(V / 2^S) * 2^S via the 1.5*2^(23+S) magic add,
+// h = V - r -- and cleared (V = r).  The decision bits are (h + 2^J - 1) / 2, accumulated per 16 stages
+// into the low mantissa bits of 2^24 + (65535 + sum).
+//
+// Lane encoding.  Position p (the trellis state rotr6(p, t%6) after stage t, as in vd_decode_sc) lives
+// in lane l = p0*1 ^ p1*2 ^ p2*7 ^ p3*8 ^ p4*16 ^ p5*32, so the butterfly partner p ^ (1<<q) is lane
+// l ^ {1, 2, 7, 8, 16, 32}[q]: DPP quad_perm (xor 1, 2), row_half_mirror (xor 7), row_ror:8 (xor 8)
+// -- each fused into the sub -- and v_permlane16_swap / v_permlane32_swap (xor 16, 32).  A swap stage
+// forms a = V + X, b = V + Y in every lane and swaps halves, after which each lane holds its own and
+// its exchanged candidate (X, Y = +-M of the lane and of its partner, from the branch-metric table).
+#pragma once
+#include "vd_kernels.h"
+
+namespace vd {
+
+template <int CH>
+struct TgFmt {
+    static_assert(CH != SOFT16, "SOFT16 metrics do not leave room for decision tags");
+    static constexpr int J = CH == HARD ? 16 : 8;  // stages per history field
+    static constexpr int S = J + 1;                // metric scale 2^S
+};
+// |metric| after the per-block renormalisation, bounded by (K-1)*(BMmax-BMmin) + 32*BMmax:
+//   HARD 12+32 = 44 < 2^(24-17);  SOFT4/FP32 192+512 = 704 < 2^15;  SOFT8 3072+8192 = 11264 < 2^15.
+
+// branch-metric table: per 96-stage group, 16 periods of 6 rows (row K = stage phase); a row holds
+// BM[L]*2^S + c*2^j for the four labels L.  M_B32 rows of phase 0 hold a second set with the other
+// tag sign (its tie rule differs between position halves there).
+template <int CORE>
+struct TgTab {
+    static constexpr int PB = CORE == B32 ? 112 : 96;  // bytes per 6-stage period
+    static __host__ __device__ constexpr int koff(int K) { return CORE == B32 ? (K == 0 ? 0 : 16 + 16 * K) : 16 * K; }
+    static __host__ __device__ constexpr int row(int r) { return (r / 6) * PB + koff(r % 6); }
+    static constexpr int BYTES = 16 * PB;
+};
+// survivor ring slots per wave: table + ring of 4 waves fit 7 workgroups per CU (<= 22.8 KiB each)
+template <int CORE>
+struct TgRing {
+    static constexpr int TBS = CORE == B32 ? 13 : 14;
+};
+
+__device__ __forceinline__ int tg_pos(int l)
+{
+    const int p2 = (l >> 2) & 1;
+    return (l & ~7) | (p2 << 2) | ((((l >> 1) & 1) ^ p2) << 1) | ((l & 1) ^ p2);
+}
+// 1 where the reference lets the own predecessor win ties (viterbiACS.cuh:113-157,216-256)
+template <int CORE>
+__device__ __forceinline__ int tg_cls(int p, int K)
+{
+    if constexpr (CORE == F16) return 1;
+    else if constexpr (CORE == B16) return 0;
+    else return (K == 0 && (p & 32)) ? 1 : 0;
+}
+// float index of position p's own-transition entry within its phase-K row
+template <int CORE>
+__device__ __forceinline__ int tg_idx(int p, int K)
+{
+    return ((CORE == B32 && K == 0) ? 4 * tg_cls<CORE>(p, K) : 0) + own_label(p, K);
+}
+
+// ---------------------------------------------------------------- stages (inline asm, exact op order)
+// DPP stage, exchange lane xor {1,2,7,8}[Q].  The DPP source (V) is >= 2 VALU slots after its write.
+template <int Q>
+__device__ __forceinline__ void tg_stage_dpp(float& V, float m)
+{
+    float t1, t2;
+#define VD_TG_DPP(CTRL)                                                                                   \
+    asm("v_add_f32 %1, %0, %3\n\ts_nop 0\n\tv_sub_f32_dpp %2, %0, %3 " CTRL " row_mask:0xf bank_mask:0xf\n\t" \
+        "v_max_f32 %0, %1, %2"                                                                           \
+        : "+v"(V), "=&v"(t1), "=&v"(t2) : "v"(m))
+    if constexpr (Q == 0) VD_TG_DPP("quad_perm:[1,0,3,2]");
+    else if constexpr (Q == 1) VD_TG_DPP("quad_perm:[2,3,0,1]");
+    else if constexpr (Q == 2) VD_TG_DPP("row_half_mirror");
+    else VD_TG_DPP("row_ror:8");
+#undef VD_TG_DPP
+}
+// swap stage, exchange lane xor 16 (Q=4) or 32 (Q=5): a = V + sx*e1, b = V - sx*e2, swap halves, max
+template <int Q>
+__device__ __forceinline__ void tg_stage_swap(float& V, float e1, float e2, float sx)
+{
+    float a, b;
+    if constexpr (Q == 4)
+        asm("v_fma_f32 %1, %3, %5, %0\n\tv_fma_f32 %2, %4, -%5, %0\n\ts_nop 1\n\t"
+            "v_permlane16_swap_b32 %1, %2\n\tv_max_f32 %0, %1, %2"
+            : "+v"(V), "=&v"(a), "=&v"(b) : "v"(e1), "v"(e2), "v"(sx));
+    else
+        asm("v_fma_f32 %1, %3, %5, %0\n\tv_fma_f32 %2, %4, -%5, %0\n\ts_nop 1\n\t"
+            "v_permlane32_swap_b32 %1, %2\n\tv_max_f32 %0, %1, %2"
+            : "+v"(V), "=&v"(a), "=&v"(b) : "v"(e1), "v"(e2), "v"(sx));
+}
+// read out and clear the history field: r = round(V / 2^S) * 2^S, h = V - r
+template <int S>
+__device__ __forceinline__ void tg_cleanup(float V, float& r, float& h)
+{
+    static_assert(S == 9 || S == 17, "magic constant");
+    if constexpr (S == 9)  // 1.5 * 2^32
+        asm("v_add_f32 %0, 0x4fc00000, %2\n\tv_subrev_f32 %0, 0x4fc00000, %0\n\tv_sub_f32 %1, %2, %0"
+            : "=&v"(r), "=&v"(h) : "v"(V));
+    else  // 1.5 * 2^40
+        asm("v_add_f32 %0, 0x53c00000, %2\n\tv_subrev_f32 %0, 0x53c00000, %0\n\tv_sub_f32 %1, %2, %0"
+            : "=&v"(r), "=&v"(h) : "v"(V));
+}
+
+// ---------------------------------------------------------------- group traceback (reference viterbiTB.cuh:4-21)
+// Ring slot = 64 words indexed by position; byte/half g of word p holds the take-bits of history field
+// g along the survivor ending at p (register exchange within the field).  Tracing word k from state
+// 0 at the end of stage 95+32k: per field, look up the bits at the position of the current state T,
+// then, with the stride-6 structure of position-space traceback (bit q_t of the position is touched
+// only by the stage-t decision, every 6 stages), the field's decoded bits are the stride-6 suffix XOR
+// of (bits ^ T << (J-6)) and the state at the field start is its low 6 bits.  M_B32 keeps its raw
+// phase-0 bits (own-wins tag in the upper position half), which already are the decoded bits there.
+// One dependent LDS read per J stages instead of one per stage.
+template <int J, bool FIX5>
+__device__ __forceinline__ uint32_t traceback_word_tg(const char* ringb, uint32_t slot1, uint64_t k)
+{
+    constexpr int G = 32 / J;
+    const int ph = (int)((2 * (k + 1)) % 6);  // stage phase of the emit block's first stage (even)
+    // position of state T at a field end of stage phase s (odd) is rotl6(T, s) = (T*65 >> (6-s)) & 63
+    int off[3];  // by s = (ph + c) % 6 for c = 1, 3, 5
+    off[0] = 5 - ph;
+    off[1] = ph <= 2 ? 3 - ph : 9 - ph;
+    off[2] = ph == 0 ? 1 : 7 - ph;
+    uint32_t m5[3] = {0u, 0u, 0u};  // M_B32: bits of phase-0 stages for field start phase ph + 2d
+    if constexpr (FIX5) {
+        sfor<3>([&](auto D) {
+            constexpr int d = decltype(D)::value;
+            m5[d] = 0x41041041u << ((12 - ph - 2 * d) % 6);
+        });
+    }
+    uint32_t T = 0, nat = 0;
+    auto field = [&](auto BOc, auto Gc, uint32_t slot) {
+        constexpr int BO = decltype(BOc)::value;  // 0: emit block, 2: convergence block
+        constexpr int g = decltype(Gc)::value;
+        constexpr int c = (BO + J * g + J - 1) % 6;
+        const uint32_t p = __builtin_amdgcn_ubfe(T * 65u, (uint32_t)off[c / 2], 6u);
+        uint32_t W;
+        if constexpr (J == 8) W = *(const uint8_t*)(ringb + slot + 4 * p + g);
+        else W = *(const uint16_t*)(ringb + slot + 4 * p + 2 * g);
+        uint32_t Y = W ^ (T << (J - 6));
+        Y ^= Y >> 6;
+        if constexpr (J == 16) Y ^= Y >> 12;
+        if constexpr (FIX5) {
+            constexpr int d = ((BO + J * g) % 6) / 2;
+            Y = (m5[d] & W) | (~m5[d] & Y);
+        }
+        T = Y & 63u;
+        return Y;
+    };
+    sfor<G>([&](auto I) {  // convergence: block k+2, fields G-1 .. 0
+        constexpr int g = G - 1 - decltype(I)::value;
+        (void)field(std::integral_constant<int, 2>{}, std::integral_constant<int, g>{}, slot1);
+    });
+    sfor<G>([&](auto I) {  // emit: block k+1
+        constexpr int g = G - 1 - decltype(I)::value;
+        nat |= field(std::integral_constant<int, 0>{}, std::integral_constant<int, g>{}, slot1 - 256u) << (J * g);
+    });
+    return __builtin_bitreverse32(nat);  // word bit i <-> stage 63+32k-i
+}
+
+// ================================================================ tagged kernel: one chunk per wave
+template <int CH, int CORE, int OB, int ABL = 0>
+__global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(7))) void vd_decode_tg(const void* __restrict__ in, void* __restrict__ out, Geom geo)
+{
+    using IN = In<CH>;
+    using TT = TgTab<CORE>;
+    constexpr int J = TgFmt<CH>::J, S = TgFmt<CH>::S;
+    constexpr int TBS = TgRing<CORE>::TBS;
+    // F16 (own wins ties everywhere) accumulates -h so the ring holds take-bits directly
+    constexpr float SG = CORE == F16 ? -1.0f : 1.0f;
+    __shared__ __attribute__((aligned(16))) char tab_all[kWaves][TT::BYTES];
+    __shared__ __attribute__((aligned(256))) uint32_t ring_all[kWaves][(TBS + 1) * 64];  // bit 31-s = stage s
+    const int lane = threadIdx.x & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int pos = tg_pos(lane);
+    char* tabb = tab_all[wv];
+    uint32_t* ring = ring_all[wv];
+    const ChunkRange cr = chunk_range(geo, blockIdx.x * kWaves + wv);
+    if (cr.words == 0) return;
+    const uint64_t t_clk0 = (ABL & 32) ? __builtin_amdgcn_s_memtime() : 0;
+    const uint64_t t_rt0 = (ABL & 32) ? __builtin_amdgcn_s_memrealtime() : 0;
+    const uint64_t start = cr.startWord * OB;
+    const uint32_t Sw = OB == 32 ? cr.words : (cr.words + 1) / 2;  // 32-bit words traced back
+    const uint32_t nblk = Sw + 2;
+
+    // per-lane LDS byte addresses of this position's table entries (row offsets are compile-time)
+    int aD[4];
+    sfor<4>([&](auto KK) {
+        constexpr int K = decltype(KK)::value + 1;
+        aD[K - 1] = 4 * tg_idx<CORE>(pos, K);
+    });
+    int a1[2], a2[2];
+    float sx[2];
+    sfor<2>([&](auto W) {
+        constexpr int w = decltype(W)::value;  // 0: K=0 (Q=5), 1: K=5 (Q=4)
+        constexpr int K = w == 0 ? 0 : 5, Q = w == 0 ? 5 : 4;
+        const int pp = pos ^ (1 << Q), bit = (pos >> Q) & 1;
+        const int io = tg_idx<CORE>(pos, K), ix = tg_idx<CORE>(pp, K);
+        a1[w] = 4 * (bit ? ix : io);
+        a2[w] = 4 * (bit ? io : ix);
+        sx[w] = bit ? -1.0f : 1.0f;
+    });
+    // table-build role: lane li writes rows li, 32+li, 64+li of each group
+    const uint64_t avail = geo.availStages;
+    const uint64_t li = (uint64_t)(lane & 31);
+    const float tagv = (float)(1 << ((int)li % J));
+    const float tg0 = CORE == F16 ? tagv : -tagv;  // tag of the row's own class
+    int rowb[3];
+    sfor<3>([&](auto R) {
+        constexpr int r = decltype(R)::value;
+        rowb[r] = TT::row(32 * r + (int)li);
+    });
+
+    float V = 0.0f;
+    uint32_t kb = 0;
+    unsigned long long* fb = nullptr;
+    unsigned long long fret = 0;
+    uint32_t fadded = 0;
+    if constexpr (!(ABL & 256)) {
+        if (geo.fair) {
+            fb = geo.fair + simd_slot();
+            if (lane == 0) atomicAdd(fb, 1ull << 32);
+        }
+    }
+    uint32_t tbn = TBS - 3 * (blockIdx.x & 3);
+    typename IN::raw_t rA = IN::load(in, start + li, avail);
+    typename IN::raw_t rB = IN::load(in, start + 32 + li, avail);
+    typename IN::raw_t rC = IN::load(in, start + 64 + li, avail);
+
+    auto block = [&](auto PHc, uint32_t j) {
+        constexpr int PH = decltype(PHc)::value;
+        constexpr int BB = PH / 2;
+        float acc = 0.0f, y0 = 0.0f, y1 = 0.0f;
+        sfor<32>([&](auto I) {
+            constexpr int i = decltype(I)::value;
+            constexpr int K = (PH + i) % 6;
+            constexpr int Q = (K + 5) % 6;
+            constexpr int ROW = TT::row(32 * BB + i);
+            if constexpr (Q <= 3) {
+                const float m = *(const float*)(tabb + aD[K - 1] + ROW);
+                tg_stage_dpp<Q>(V, m);
+            } else {
+                constexpr int w = K == 0 ? 0 : 1;
+                const float e1 = *(const float*)(tabb + a1[w] + ROW);
+                const float e2 = *(const float*)(tabb + a2[w] + ROW);
+                tg_stage_swap<Q>(V, e1, e2, sx[w]);
+            }
+            if constexpr (i % J == J - 1) {
+                float r, h;
+                tg_cleanup<S>(V, r, h);
+                V = r;
+                if constexpr ((i % 16) / J == 0) acc = 65535.0f + SG * h;
+                else acc = __builtin_fmaf(h, SG * 256.0f, acc);
+                if constexpr (i % 16 == 15) {
+                    if constexpr (i < 16) y0 = acc + 16777216.0f;
+                    else y1 = acc + 16777216.0f;
+                }
+            }
+        });
+        // ring word of position p: byte (J=8) / half (J=16) g = the J path bits of the survivor that
+        // ends at p at the end of history field g of this block, stage 8g+j (16g+j) at bit j of it
+        const uint32_t word =
+            __builtin_amdgcn_perm(__builtin_bit_cast(uint32_t, y1), __builtin_bit_cast(uint32_t, y0), 0x05040100u);
+        // decision-neutral renormalisation by the metric of position 0 (V is a multiple of 2^S here)
+        V -= __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, V)));
+        if constexpr (ABL & 64) ((uint32_t*)out + (1u << 20))[j * 64 + pos] = word;  // tools: ring words
+        wave_sync();
+        if (j >= 1) ring[(j - 1 - kb) * 64 + pos] = word;
+        if (j >= 2 && (j - 1 - kb == tbn || j == nblk - 1)) {
+            wave_sync();
+            const uint32_t nw = j - 1 - kb;
+            if (!(ABL & 1) && (uint32_t)lane < nw) {
+                const uint64_t k = kb + lane;
+                const uint32_t Q0 = (uint32_t)(wv * (TBS + 1) * 256 + (lane + 1) * 256);
+                uint32_t w = traceback_word_tg<J, CORE == B32>((const char*)ring_all, Q0, k);
+                if constexpr (OB == 32) {
+                    ((uint32_t*)out)[cr.startWord + k] = w;
+                } else {
+                    uint16_t* o = (uint16_t*)out + cr.startWord;
+                    o[2 * k] = (uint16_t)(w >> 16);
+                    if (2 * k + 1 < cr.words) o[2 * k + 1] = (uint16_t)(w & 0xFFFF);
+                }
+            }
+            wave_sync();
+            ring[pos] = word;  // block j becomes slot 0 of the next batch
+            kb = j - 1;
+            tbn = TBS;
+        }
+        return j + 1 < nblk;
+    };
+    // one 96-stage group's table row from the stage's (A, B) = (BM[3], BM[2])
+    auto put_row = [&](int rb, int A, int B, int r6) {
+        constexpr float SC = (float)(1 << S);
+        const float af = (float)A, bf = (float)B;
+        float4 e = make_float4(__builtin_fmaf(af, -SC, tg0), __builtin_fmaf(bf, -SC, tg0),
+                               __builtin_fmaf(bf, SC, tg0), __builtin_fmaf(af, SC, tg0));
+        *(float4*)(tabb + rb) = e;
+        if constexpr (CORE == B32) {
+            if (r6 == 0)  // phase-0 row: the own-wins set (+tag) for the upper position half
+                *(float4*)(tabb + rb + 16) = make_float4(__builtin_fmaf(af, -SC, tagv), __builtin_fmaf(bf, -SC, tagv),
+                                                          __builtin_fmaf(bf, SC, tagv), __builtin_fmaf(af, SC, tagv));
+        }
+    };
+    const int r6a = (int)li % 6, r6b = (int)(li + 32) % 6, r6c = (int)(li + 64) % 6;
+    for (uint32_t j = 0;; j += 3) {
+        if constexpr (!(ABL & 256)) {
+            if (fb) {
+                if (j > 0) {
+                    const uint64_t r = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(fret >> 32)) << 32) |
+                                       (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)fret);
+                    const int64_t n = (int64_t)(r >> 32), sum = (int64_t)(uint32_t)r + 3;
+                    const int64_t d = (int64_t)j * n - sum;
+                    if (d <= -3 * n) __builtin_amdgcn_s_setprio(3);
+                    else if (d <= 0) __builtin_amdgcn_s_setprio(2);
+                    else if (d <= 3 * n) __builtin_amdgcn_s_setprio(1);
+                    else __builtin_amdgcn_s_setprio(0);
+                }
+                if (lane == 0) fret = atomicAdd(fb, 3ull);
+                fadded += 3;
+            }
+        }
+        if (lane < 32) {
+            int A, B;
+            IN::ab(rA, start + 32ull * j + li, avail, A, B);
+            put_row(rowb[0], A, B, r6a);
+            IN::ab(rB, start + 32ull * (j + 1) + li, avail, A, B);
+            put_row(rowb[1], A, B, r6b);
+            IN::ab(rC, start + 32ull * (j + 2) + li, avail, A, B);
+            put_row(rowb[2], A, B, r6c);
+        }
+        if constexpr (!(ABL & 16)) {
+            rA = IN::load(in, start + 32ull * (j + 3) + li, avail);
+            rB = IN::load(in, start + 32ull * (j + 4) + li, avail);
+            rC = IN::load(in, start + 32ull * (j + 5) + li, avail);
+        }
+        wave_sync();
+        if (!block(std::integral_constant<int, 0>{}, j)) break;
+        if (!block(std::integral_constant<int, 2>{}, j + 1)) break;
+        if (!block(std::integral_constant<int, 4>{}, j + 2)) break;
+        wave_sync();
+    }
+    if constexpr (!(ABL & 256)) {
+        if (fb && lane == 0) atomicAdd(fb, 0ull - ((1ull << 32) + fadded));
+    }
+    if constexpr (ABL & 32) {
+        const uint64_t c1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+        if (lane == 0) {
+            uint64_t* d = (uint64_t*)((char*)out + (16u << 20)) + 6 * (blockIdx.x * kWaves + wv);
+            d[0] = t_clk0; d[1] = c1; d[2] = t_rt0; d[3] = r1;
+            d[4] = (uint32_t)__builtin_amdgcn_s_getreg(4 | (0 << 6) | (31 << 11));
+            d[5] = (uint32_t)__builtin_amdgcn_s_getreg(20 | (0 << 6) | (31 << 11));
+        }
+    }
+}
+
+}  // namespace vd

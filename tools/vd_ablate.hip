@@ -7,6 +7,7 @@
 #include <vector>
 #include <algorithm>
 #include "../gpu-accelerated-viterbi-decoder_amd/csrc/vd_kernels.h"
+#include "../gpu-accelerated-viterbi-decoder_amd/csrc/vd_kernel_tg.h"
 
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP error %s at %d\n", hipGetErrorString(e), __LINE__); exit(1); } } while (0)
 
@@ -15,12 +16,15 @@ struct Var { const char* name; KFn fn; int grid; int block = 256; };
 
 template <int ABL> void addb(std::vector<Var>& v, const char* n) { v.push_back({n, (KFn)vd::vd_decode_sc<vd::HARD, vd::B32, 32, ABL>, 1600}); }
 template <int ABL> void adds(std::vector<Var>& v, const char* n) { v.push_back({n, (KFn)vd::vd_decode_sc<vd::SOFT8, vd::B16, 32, ABL>, 1600}); }
+template <int ABL> void tgb(std::vector<Var>& v, const char* n) { v.push_back({n, (KFn)vd::vd_decode_tg<vd::HARD, vd::B32, 32, ABL>, 1600}); }
+template <int ABL> void tgs(std::vector<Var>& v, const char* n) { v.push_back({n, (KFn)vd::vd_decode_tg<vd::SOFT8, vd::B16, 32, ABL>, 1600}); }
+template <int ABL> void tgf(std::vector<Var>& v, const char* n) { v.push_back({n, (KFn)vd::vd_decode_tg<vd::FP32, vd::F16, 32, ABL>, 1600}); }
 template <int ABL> void addp(std::vector<Var>& v, const char* n) { v.push_back({n, (KFn)vd::vd_decode_pk<vd::SOFT8, vd::B16, 32, ABL>, 3200, 64}); }
 
 int main(int argc, char** argv)
 {
     const size_t N = 32000000, inputNum = 2 * N;
-    const size_t inBytes = inputNum;  // SOFT8 (largest of the two)
+    const size_t inBytes = inputNum * 4;  // FP32 (largest)
     void *in, *out;
     CK(hipMalloc(&in, inBytes));
     CK(hipMalloc(&out, (16u << 20) + 6400 * 48));
@@ -39,7 +43,8 @@ int main(int argc, char** argv)
     addb<4>(v, "sc hard/b32 -bmread"); addb<8>(v, "sc hard/b32 -decisions"); addb<15>(v, "sc hard/b32 skeleton");
     addb<16>(v, "sc hard/b32 -loads"); addb<17>(v, "sc hard/b32 -loads-traceback"); addb<31>(v, "sc hard/b32 skel-loads"); addb<256>(v, "sc hard/b32 -fairness"); adds<256>(v, "sc soft8/b16 -fairness");
     adds<0>(v, "sc soft8/b16 full"); adds<1>(v, "sc soft8/b16 -traceback"); adds<16>(v, "sc soft8/b16 -loads");
-    addp<0>(v, "pk soft8/b16 full"); addp<1>(v, "pk soft8/b16 -traceback");
+    tgb<0>(v, "tg hard/b32 full"); tgb<1>(v, "tg hard/b32 -traceback"); tgb<16>(v, "tg hard/b32 -loads"); tgb<256>(v, "tg hard/b32 -fairness");
+    tgs<0>(v, "tg soft8/b16 full"); tgs<1>(v, "tg soft8/b16 -traceback"); tgs<256>(v, "tg soft8/b16 -fairness"); tgf<0>(v, "tg fp32/f16 full");
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
     const int rounds = argc > 1 ? atoi(argv[1]) : 10;
@@ -59,8 +64,8 @@ int main(int argc, char** argv)
                (double)(N - 64) / (t[i][t[i].size() / 2] * 1e-3) / 1e9);
     }
     // per-wave clock stamps of the full kernel (ABL 32), without and with the priority schedule (64)
-    for (KFn f : {(KFn)vd::vd_decode_sc<vd::HARD, vd::B32, 32, 32>, (KFn)vd::vd_decode_sc<vd::HARD, vd::B32, 32, 288>}) {
-        printf("=== %s\n", f == (KFn)vd::vd_decode_sc<vd::HARD, vd::B32, 32, 32> ? "full" : "full -fairness");
+    for (KFn f : {(KFn)vd::vd_decode_sc<vd::HARD, vd::B32, 32, 32>, (KFn)vd::vd_decode_tg<vd::HARD, vd::B32, 32, 32>}) {
+        printf("=== %s\n", f == (KFn)vd::vd_decode_sc<vd::HARD, vd::B32, 32, 32> ? "sc full" : "tg full");
         for (int r = 0; r < 3; r++) hipLaunchKernelGGL(f, dim3(1600), dim3(256), 0, 0, in, out, g);
         CK(hipDeviceSynchronize());
         std::vector<uint64_t> d(6400 * 6);

@@ -1,0 +1,44 @@
+// vd_tgdump.hip -- debugging aid (tools only): decodes one packed HARD/B32 input as ONE chunk with
+// vd_decode_tg and dumps the decoded words and every ring word (block j, position p) to a file.
+// usage: vd_tgdump in.bin out.bin  (in.bin = packed HARD words; N = 16 * words stages)
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+#include "../gpu-accelerated-viterbi-decoder_amd/csrc/vd_kernel_tg.h"
+#define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP error %s at %d\n", hipGetErrorString(e), __LINE__); exit(1); } } while (0)
+int main(int argc, char** argv)
+{
+    FILE* f = fopen(argv[1], "rb");
+    std::vector<uint32_t> in(1 << 22);
+    size_t nw = fread(in.data(), 4, in.size(), f);
+    fclose(f);
+    const uint64_t stages = nw * 16;
+    vd::Geom g;
+    g.packNum = (stages - 64) / 32;
+    g.availStages = stages;
+    g.nchunks = argc > 3 ? atoi(argv[3]) : 1;
+    g.fair = nullptr;
+    const int fair = argc > 4 ? atoi(argv[4]) : 0;
+    if (fair) { CK(hipMalloc(&g.fair, vd::kFairSlots * 8)); CK(hipMemset(g.fair, 0, vd::kFairSlots * 8)); }
+    void *din, *dout;
+    CK(hipMalloc(&din, nw * 4));
+    CK(hipMalloc(&dout, (8u << 20)));
+    CK(hipMemset(dout, 0, 8u << 20));
+    CK(hipMemcpy(din, in.data(), nw * 4, hipMemcpyHostToDevice));
+    const dim3 grid((g.nchunks + 3) / 4);
+    if (g.nchunks == 1)
+        hipLaunchKernelGGL((vd::vd_decode_tg<vd::HARD, vd::B32, 32, 64 | 256>), grid, dim3(256), 0, 0, din, dout, g);
+    else
+        hipLaunchKernelGGL((vd::vd_decode_tg<vd::HARD, vd::B32, 32, 0>), grid, dim3(256), 0, 0, din, dout, g);
+    CK(hipDeviceSynchronize());
+    std::vector<uint32_t> h(2u << 20);
+    CK(hipMemcpy(h.data(), dout, 8u << 20, hipMemcpyDeviceToHost));
+    FILE* o = fopen(argv[2], "wb");
+    fwrite(&g.packNum, 8, 1, o);
+    fwrite(h.data(), 4, g.packNum, o);                         // decoded words
+    if (g.nchunks == 1) fwrite(h.data() + (1u << 20), 4, (g.packNum + 2) * 64, o);  // ring words
+    fclose(o);
+    printf("packNum %llu\n", (unsigned long long)g.packNum);
+    return 0;
+}
