@@ -38,12 +38,17 @@ struct TgFmt {
 
 // branch-metric table: per 96-stage group, 16 periods of 6 rows (row K = stage phase); a row holds
 // BM[L]*2^S + c*2^j for the four labels L.  M_B32 rows of phase 0 hold a second set with the other
-// tag sign (its tie rule differs between position halves there).
+// tag sign (its tie rule differs between position halves there).  Rows K of periods 2m and 2m+1 are
+// interleaved entry by entry, so a lane's entries for stages t and t+6 are one 8-byte ds_read_b64:
+// entry e of row r sits at row(r) + 8e.
 template <int CORE>
 struct TgTab {
     static constexpr int PB = CORE == B32 ? 112 : 96;  // bytes per 6-stage period
     static __host__ __device__ constexpr int koff(int K) { return CORE == B32 ? (K == 0 ? 0 : 16 + 16 * K) : 16 * K; }
-    static __host__ __device__ constexpr int row(int r) { return (r / 6) * PB + koff(r % 6); }
+    static __host__ __device__ constexpr int row(int r)
+    {
+        return (r / 12) * 2 * PB + 2 * koff(r % 6) + 4 * ((r / 6) % 2);
+    }
     static constexpr int BYTES = 16 * PB;
 };
 // survivor ring slots per wave: table + ring of 4 waves fit 7 workgroups per CU (<= 22.8 KiB each)
@@ -171,11 +176,104 @@ __device__ __forceinline__ uint32_t traceback_word_tg(const char* ringb, uint32_
     return __builtin_bitreverse32(nat);  // word bit i <-> stage 63+32k-i
 }
 
+// ---------------------------------------------------------------- channel input through a buffer resource
+// Formats as In<CH> (viterbiBM.cuh:15-153).  The resource of a 96-stage group starts at the group's
+// first stage and ends at the last whole word of the caller's data, so reads past the input return
+// zero -- the reference window's "no data" -- with no per-lane address or range arithmetic.  Row r of
+// the group (stage 32r + li) reads at voff(li) + r * RB.
+template <int CH>
+struct TgIn;
+template <>
+struct TgIn<HARD> {  // 16 stages per word; stage g -> bits 31-2(g%16), 30-2(g%16); g%16 = li%16
+    using raw_t = uint32_t;
+    static constexpr int RB = 8;
+    static __device__ __forceinline__ uint64_t bytes(uint64_t stages) { return stages / 4; }
+    static __device__ __forceinline__ uint32_t voff(int li) { return 4u * (uint32_t)(li >> 4); }
+    template <int R>
+    static __device__ __forceinline__ raw_t load(__amdgpu_buffer_rsrc_t rs, uint32_t vo)
+    {
+        return __builtin_amdgcn_raw_buffer_load_b32(rs, vo + R * RB, 0, 0);
+    }
+    static __device__ __forceinline__ void ab(raw_t w, int li, int& A, int& B)
+    {
+        const int sh = 30 - 2 * (li & 15);
+        const int r0 = (w >> (sh + 1)) & 1, r1 = (w >> sh) & 1;
+        A = r0 + r1 - 1;
+        B = r0 - r1;
+    }
+};
+template <>
+struct TgIn<SOFT4> {  // 4 stages per word, byte g%4 from the MSB: high nibble s0, low nibble s1
+    using raw_t = uint32_t;
+    static constexpr int RB = 32;
+    static __device__ __forceinline__ uint64_t bytes(uint64_t stages) { return stages; }
+    static __device__ __forceinline__ uint32_t voff(int li) { return 4u * (uint32_t)(li >> 2); }
+    template <int R>
+    static __device__ __forceinline__ raw_t load(__amdgpu_buffer_rsrc_t rs, uint32_t vo)
+    {
+        return __builtin_amdgcn_raw_buffer_load_b32(rs, vo + R * RB, 0, 0);
+    }
+    static __device__ __forceinline__ void ab(raw_t w, int li, int& A, int& B)
+    {
+        const int sh = 24 - 8 * (li & 3);
+        const int s0 = (int)(w << (24 - sh)) >> 28, s1 = (int)(w << (28 - sh)) >> 28;
+        A = s0 + s1;
+        B = s0 - s1;
+    }
+};
+template <>
+struct TgIn<SOFT8> {  // 2 stages per word; the 16-bit half g^1 holds s0 (high byte), s1 (low byte)
+    using raw_t = uint32_t;
+    static constexpr int RB = 64;
+    static __device__ __forceinline__ uint64_t bytes(uint64_t stages) { return stages * 2; }
+    static __device__ __forceinline__ uint32_t voff(int li) { return 2u * (uint32_t)(li ^ 1); }
+    template <int R>
+    static __device__ __forceinline__ raw_t load(__amdgpu_buffer_rsrc_t rs, uint32_t vo)
+    {
+        return (uint32_t)__builtin_amdgcn_raw_buffer_load_b16(rs, vo + R * RB, 0, 0);
+    }
+    static __device__ __forceinline__ void ab(raw_t w, int, int& A, int& B)
+    {
+        const int s0 = (int)(w << 16) >> 24, s1 = (int)(w << 24) >> 24;
+        A = s0 + s1;
+        B = s0 - s1;
+    }
+};
+template <>
+struct TgIn<FP32> {  // 2 floats per stage, clamped to [-8,7]; BM = (int)(+-x0 +- x1) (truncation)
+    using raw_t = float2;
+    static constexpr int RB = 256;
+    static __device__ __forceinline__ uint64_t bytes(uint64_t stages) { return stages * 8; }
+    static __device__ __forceinline__ uint32_t voff(int li) { return 8u * (uint32_t)li; }
+    template <int R>
+    static __device__ __forceinline__ raw_t load(__amdgpu_buffer_rsrc_t rs, uint32_t vo)
+    {
+        typedef float f2 __attribute__((ext_vector_type(2)));
+        const f2 v = __builtin_bit_cast(f2, __builtin_amdgcn_raw_buffer_load_b64(rs, vo + R * RB, 0, 0));
+        return make_float2(v.x, v.y);
+    }
+    static __device__ __forceinline__ void ab(raw_t v, int, int& A, int& B)
+    {
+        const float x0 = fminf(fmaxf(v.x, -8.0f), 7.0f), x1 = fminf(fmaxf(v.y, -8.0f), 7.0f);
+        A = (int)__fadd_rn(x0, x1);
+        B = (int)__fsub_rn(x0, x1);
+    }
+};
+// resource for the 96 stages from g0 (g0 a multiple of 16; inputs below 4 GiB)
+template <int CH>
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t tg_rsrc(const void* in, uint64_t g0, uint64_t availBytes)
+{
+    const uint64_t off = TgIn<CH>::bytes(g0);
+    const uint64_t rem = availBytes > off ? availBytes - off : 0;
+    return __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)in + off), (short)0,
+                                             (int)(uint32_t)(rem < 0xFFFFFFFFull ? rem : 0xFFFFFFFFull), 0x00020000);
+}
+
 // ================================================================ tagged kernel: one chunk per wave
 template <int CH, int CORE, int OB, int ABL = 0>
 __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(7))) void vd_decode_tg(const void* __restrict__ in, void* __restrict__ out, Geom geo)
 {
-    using IN = In<CH>;
+    using IN = TgIn<CH>;
     using TT = TgTab<CORE>;
     constexpr int J = TgFmt<CH>::J, S = TgFmt<CH>::S;
     constexpr int TBS = TgRing<CORE>::TBS;
@@ -200,7 +298,7 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(7))
     int aD[4];
     sfor<4>([&](auto KK) {
         constexpr int K = decltype(KK)::value + 1;
-        aD[K - 1] = 4 * tg_idx<CORE>(pos, K);
+        aD[K - 1] = 8 * tg_idx<CORE>(pos, K);
     });
     int a1[2], a2[2];
     float sx[2];
@@ -209,8 +307,8 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(7))
         constexpr int K = w == 0 ? 0 : 5, Q = w == 0 ? 5 : 4;
         const int pp = pos ^ (1 << Q), bit = (pos >> Q) & 1;
         const int io = tg_idx<CORE>(pos, K), ix = tg_idx<CORE>(pp, K);
-        a1[w] = 4 * (bit ? ix : io);
-        a2[w] = 4 * (bit ? io : ix);
+        a1[w] = 8 * (bit ? ix : io);
+        a2[w] = 8 * (bit ? io : ix);
         sx[w] = bit ? -1.0f : 1.0f;
     });
     // table-build role: lane li writes rows li, 32+li, 64+li of each group
@@ -236,10 +334,14 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(7))
         }
     }
     uint32_t tbn = TBS - 3 * (blockIdx.x & 3);
-    typename IN::raw_t rA = IN::load(in, start + li, avail);
-    typename IN::raw_t rB = IN::load(in, start + 32 + li, avail);
-    typename IN::raw_t rC = IN::load(in, start + 64 + li, avail);
+    const uint64_t availB = IN::bytes(avail);
+    const uint32_t vo = IN::voff((int)li);
+    __amdgpu_buffer_rsrc_t rs = tg_rsrc<CH>(in, start, availB);
+    typename IN::raw_t rA = IN::template load<0>(rs, vo);
+    typename IN::raw_t rB = IN::template load<1>(rs, vo);
+    typename IN::raw_t rC = IN::template load<2>(rs, vo);
 
+    float kD[6], k1[2], k2[2];  // table entries read 6 stages ahead (next period)
     auto block = [&](auto PHc, uint32_t j) {
         constexpr int PH = decltype(PHc)::value;
         constexpr int BB = PH / 2;
@@ -248,17 +350,30 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(7))
             constexpr int i = decltype(I)::value;
             constexpr int K = (PH + i) % 6;
             constexpr int Q = (K + 5) % 6;
-            constexpr int ROW = TT::row(32 * BB + i);
-            if constexpr (Q <= 3) {
-                const float m = *(const float*)(tabb + aD[K - 1] + ROW);
-                tg_stage_dpp<Q>(V, m);
+            constexpr int r = 32 * BB + i;  // stage within the group
+            constexpr bool EVEN = (r / 6) % 2 == 0;
+            constexpr int ROWE = TT::row(r) & ~4;  // entry pair of periods 2m, 2m+1
+            // one ds_read_b64 at the even period serves this stage and the one 6 stages later
+            auto rd = [&](int a, float& keep) -> float {
+                if constexpr (EVEN) {
+                    const float2 v = *(const float2*)(tabb + a + ROWE);
+                    keep = v.y;
+                    return v.x;
+                } else {
+                    return keep;
+                }
+            };
+            // ABL (tools only): 2 = no table reads, 128 = every stage a DPP stage, 4 = no field read-out
+            if constexpr (Q <= 3 || (ABL & 128)) {
+                const float m = (ABL & 2) ? (float)aD[(K + 3) % 4] : rd(aD[(K + 3) % 4], kD[K]);
+                tg_stage_dpp<(Q <= 3 ? Q : 3)>(V, m);
             } else {
                 constexpr int w = K == 0 ? 0 : 1;
-                const float e1 = *(const float*)(tabb + a1[w] + ROW);
-                const float e2 = *(const float*)(tabb + a2[w] + ROW);
+                const float e1 = (ABL & 2) ? (float)a1[w] : rd(a1[w], k1[w]);
+                const float e2 = (ABL & 2) ? (float)a2[w] : rd(a2[w], k2[w]);
                 tg_stage_swap<Q>(V, e1, e2, sx[w]);
             }
-            if constexpr (i % J == J - 1) {
+            if constexpr (i % J == J - 1 && !(ABL & 4)) {
                 float r, h;
                 tg_cleanup<S>(V, r, h);
                 V = r;
@@ -305,17 +420,45 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(7))
     auto put_row = [&](int rb, int A, int B, int r6) {
         constexpr float SC = (float)(1 << S);
         const float af = (float)A, bf = (float)B;
-        float4 e = make_float4(__builtin_fmaf(af, -SC, tg0), __builtin_fmaf(bf, -SC, tg0),
-                               __builtin_fmaf(bf, SC, tg0), __builtin_fmaf(af, SC, tg0));
-        *(float4*)(tabb + rb) = e;
+        float* e = (float*)(tabb + rb);
+        if constexpr (ABL & 512) {  // tools only: compute the row, do not store it
+            float x0 = __builtin_fmaf(af, -SC, tg0), x1 = __builtin_fmaf(bf, -SC, tg0);
+            float x2 = __builtin_fmaf(bf, SC, tg0), x3 = __builtin_fmaf(af, SC, tg0);
+            asm volatile("" ::"v"(x0), "v"(x1), "v"(x2), "v"(x3));
+            return;
+        }
+        e[0] = __builtin_fmaf(af, -SC, tg0);
+        e[2] = __builtin_fmaf(bf, -SC, tg0);
+        e[4] = __builtin_fmaf(bf, SC, tg0);
+        e[6] = __builtin_fmaf(af, SC, tg0);
         if constexpr (CORE == B32) {
-            if (r6 == 0)  // phase-0 row: the own-wins set (+tag) for the upper position half
-                *(float4*)(tabb + rb + 16) = make_float4(__builtin_fmaf(af, -SC, tagv), __builtin_fmaf(bf, -SC, tagv),
-                                                          __builtin_fmaf(bf, SC, tagv), __builtin_fmaf(af, SC, tagv));
+            if (r6 == 0) {  // phase-0 row: the own-wins set (+tag) for the upper position half
+                e[8] = __builtin_fmaf(af, -SC, tagv);
+                e[10] = __builtin_fmaf(bf, -SC, tagv);
+                e[12] = __builtin_fmaf(bf, SC, tagv);
+                e[14] = __builtin_fmaf(af, SC, tagv);
+            }
         }
     };
     const int r6a = (int)li % 6, r6b = (int)(li + 32) % 6, r6c = (int)(li + 64) % 6;
     for (uint32_t j = 0;; j += 3) {
+        // group head: the table from the inputs loaded one group ago, the next group's loads, then the
+        // fairness board (its atomic returns during this group; nothing here waits on it)
+        if (lane < 32 && !(ABL & 8)) {  // ABL 8 (tools only): no table build
+            int A, B;
+            IN::ab(rA, (int)li, A, B);
+            put_row(rowb[0], A, B, r6a);
+            IN::ab(rB, (int)li, A, B);
+            put_row(rowb[1], A, B, r6b);
+            IN::ab(rC, (int)li, A, B);
+            put_row(rowb[2], A, B, r6c);
+        }
+        if constexpr (!(ABL & 16)) {
+            rs = tg_rsrc<CH>(in, start + 32ull * (j + 3), availB);
+            rA = IN::template load<0>(rs, vo);
+            rB = IN::template load<1>(rs, vo);
+            rC = IN::template load<2>(rs, vo);
+        }
         if constexpr (!(ABL & 256)) {
             if (fb) {
                 if (j > 0) {
@@ -331,20 +474,6 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(7))
                 if (lane == 0) fret = atomicAdd(fb, 3ull);
                 fadded += 3;
             }
-        }
-        if (lane < 32) {
-            int A, B;
-            IN::ab(rA, start + 32ull * j + li, avail, A, B);
-            put_row(rowb[0], A, B, r6a);
-            IN::ab(rB, start + 32ull * (j + 1) + li, avail, A, B);
-            put_row(rowb[1], A, B, r6b);
-            IN::ab(rC, start + 32ull * (j + 2) + li, avail, A, B);
-            put_row(rowb[2], A, B, r6c);
-        }
-        if constexpr (!(ABL & 16)) {
-            rA = IN::load(in, start + 32ull * (j + 3) + li, avail);
-            rB = IN::load(in, start + 32ull * (j + 4) + li, avail);
-            rC = IN::load(in, start + 32ull * (j + 5) + li, avail);
         }
         wave_sync();
         if (!block(std::integral_constant<int, 0>{}, j)) break;

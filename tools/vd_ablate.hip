@@ -39,12 +39,12 @@ int main(int argc, char** argv)
     CK(hipMalloc(&g.fair, vd::kFairSlots * 8));
     CK(hipMemset(g.fair, 0, vd::kFairSlots * 8));
     std::vector<Var> v;
-    addb<0>(v, "sc hard/b32 full"); addb<1>(v, "sc hard/b32 -traceback"); addb<2>(v, "sc hard/b32 lds-xchg->dpp");
-    addb<4>(v, "sc hard/b32 -bmread"); addb<8>(v, "sc hard/b32 -decisions"); addb<15>(v, "sc hard/b32 skeleton");
-    addb<16>(v, "sc hard/b32 -loads"); addb<17>(v, "sc hard/b32 -loads-traceback"); addb<31>(v, "sc hard/b32 skel-loads"); addb<256>(v, "sc hard/b32 -fairness"); adds<256>(v, "sc soft8/b16 -fairness");
-    adds<0>(v, "sc soft8/b16 full"); adds<1>(v, "sc soft8/b16 -traceback"); adds<16>(v, "sc soft8/b16 -loads");
+    addb<0>(v, "sc hard/b32 full"); addb<1>(v, "sc hard/b32 -traceback");
+    adds<0>(v, "sc soft8/b16 full");
     tgb<0>(v, "tg hard/b32 full"); tgb<1>(v, "tg hard/b32 -traceback"); tgb<16>(v, "tg hard/b32 -loads"); tgb<256>(v, "tg hard/b32 -fairness");
-    tgs<0>(v, "tg soft8/b16 full"); tgs<1>(v, "tg soft8/b16 -traceback"); tgs<256>(v, "tg soft8/b16 -fairness"); tgf<0>(v, "tg fp32/f16 full");
+    tgb<2>(v, "tg hard/b32 -tabreads"); tgb<4>(v, "tg hard/b32 -readout"); tgb<8>(v, "tg hard/b32 -tabbuild"); tgb<128>(v, "tg hard/b32 all-dpp"); tgb<512>(v, "tg hard/b32 -tabwrites"); tgs<512>(v, "tg soft8/b16 -tabwrites"); tgs<8>(v, "tg soft8/b16 -tabbuild");
+    tgb<2 | 4 | 8 | 16 | 1>(v, "tg hard/b32 ACS only"); tgb<2 | 4 | 8 | 16 | 1 | 128>(v, "tg hard/b32 ACS only all-dpp");
+    tgs<0>(v, "tg soft8/b16 full"); tgs<1>(v, "tg soft8/b16 -traceback"); tgs<2>(v, "tg soft8/b16 -tabreads"); tgs<4>(v, "tg soft8/b16 -readout"); tgf<0>(v, "tg fp32/f16 full");
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
     const int rounds = argc > 1 ? atoi(argv[1]) : 10;
