@@ -341,7 +341,36 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(7))
     typename IN::raw_t rB = IN::template load<1>(rs, vo);
     typename IN::raw_t rC = IN::template load<2>(rs, vo);
 
-    float kD[6], k1[2], k2[2];  // table entries read 6 stages ahead (next period)
+    // Branch-metric table reads, software-pipelined: the entries of stage r are loaded TGD stages
+    // ahead; one ds_read_b64 at an even period also carries the entry of the stage 6 later.  The
+    // loads are volatile LDS-address-space loads so they stay single ds_read_b64s (2 LDS cycles) in
+    // program order -- left alone the compiler merges neighbours into ds_read2_b64 (8 cycles).
+    constexpr int TGD = 4;
+    typedef float f2v __attribute__((ext_vector_type(2)));
+    typedef __attribute__((address_space(3))) const volatile f2v* lptr;
+    const __attribute__((address_space(3))) char* tl = (const __attribute__((address_space(3))) char*)tabb;
+    float va[96], vb[96];
+    auto issue = [&](auto Rc) {
+        constexpr int r = decltype(Rc)::value;  // stage within the group (the group starts at phase 0)
+        if constexpr ((r / 6) % 2 == 0 && !(ABL & 2)) {
+            constexpr int K = r % 6;
+            constexpr int Q = (K + 5) % 6;
+            constexpr int ROWE = TT::row(r);
+            if constexpr (Q <= 3 || (ABL & 128)) {
+                const f2v v = *(lptr)(tl + aD[(K + 3) % 4] + ROWE);
+                va[r] = v.x;
+                va[r + 6] = v.y;
+            } else {
+                constexpr int w = K == 0 ? 0 : 1;
+                const f2v v1 = *(lptr)(tl + a1[w] + ROWE);
+                const f2v v2 = *(lptr)(tl + a2[w] + ROWE);
+                va[r] = v1.x;
+                va[r + 6] = v1.y;
+                vb[r] = v2.x;
+                vb[r + 6] = v2.y;
+            }
+        }
+    };
     auto block = [&](auto PHc, uint32_t j) {
         constexpr int PH = decltype(PHc)::value;
         constexpr int BB = PH / 2;
@@ -351,32 +380,21 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(7))
             constexpr int K = (PH + i) % 6;
             constexpr int Q = (K + 5) % 6;
             constexpr int r = 32 * BB + i;  // stage within the group
-            constexpr bool EVEN = (r / 6) % 2 == 0;
-            constexpr int ROWE = TT::row(r) & ~4;  // entry pair of periods 2m, 2m+1
-            // one ds_read_b64 at the even period serves this stage and the one 6 stages later
-            auto rd = [&](int a, float& keep) -> float {
-                if constexpr (EVEN) {
-                    const float2 v = *(const float2*)(tabb + a + ROWE);
-                    keep = v.y;
-                    return v.x;
-                } else {
-                    return keep;
-                }
-            };
             // ABL (tools only): 2 = no table reads, 128 = every stage a DPP stage, 4 = no field read-out
             if constexpr (Q <= 3 || (ABL & 128)) {
-                const float m = (ABL & 2) ? (float)aD[(K + 3) % 4] : rd(aD[(K + 3) % 4], kD[K]);
+                const float m = (ABL & 2) ? (float)aD[(K + 3) % 4] : va[r];
                 tg_stage_dpp<(Q <= 3 ? Q : 3)>(V, m);
             } else {
                 constexpr int w = K == 0 ? 0 : 1;
-                const float e1 = (ABL & 2) ? (float)a1[w] : rd(a1[w], k1[w]);
-                const float e2 = (ABL & 2) ? (float)a2[w] : rd(a2[w], k2[w]);
+                const float e1 = (ABL & 2) ? (float)a1[w] : va[r];
+                const float e2 = (ABL & 2) ? (float)a2[w] : vb[r];
                 tg_stage_swap<Q>(V, e1, e2, sx[w]);
             }
+            if constexpr (r + TGD < 96) issue(std::integral_constant<int, r + TGD>{});
             if constexpr (i % J == J - 1 && !(ABL & 4)) {
-                float r, h;
-                tg_cleanup<S>(V, r, h);
-                V = r;
+                float vr, h;
+                tg_cleanup<S>(V, vr, h);
+                V = vr;
                 if constexpr ((i % 16) / J == 0) acc = 65535.0f + SG * h;
                 else acc = __builtin_fmaf(h, SG * 256.0f, acc);
                 if constexpr (i % 16 == 15) {
@@ -476,6 +494,7 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(7))
             }
         }
         wave_sync();
+        sfor<TGD>([&](auto X) { issue(X); });
         if (!block(std::integral_constant<int, 0>{}, j)) break;
         if (!block(std::integral_constant<int, 2>{}, j + 1)) break;
         if (!block(std::integral_constant<int, 4>{}, j + 2)) break;
