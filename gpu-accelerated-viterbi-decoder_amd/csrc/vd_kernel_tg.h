@@ -313,14 +313,12 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(7))
     });
     // table-build role: lane li writes rows li, 32+li, 64+li of each group
     const uint64_t avail = geo.availStages;
+    // table-build roles: every lane writes row `lane` (stages 0..63 of the group), lanes 0..31 also
+    // row 64 + lane; J divides 32, so the tag position (row % J) is lane % J for both
     const uint64_t li = (uint64_t)(lane & 31);
-    const float tagv = (float)(1 << ((int)li % J));
+    const float tagv = (float)(1 << (lane % J));
     const float tg0 = CORE == F16 ? tagv : -tagv;  // tag of the row's own class
-    int rowb[3];
-    sfor<3>([&](auto R) {
-        constexpr int r = decltype(R)::value;
-        rowb[r] = TT::row(32 * r + (int)li);
-    });
+    const int rowb1 = TT::row(lane), rowb2 = TT::row(64 + (int)li);
 
     float V = 0.0f;
     uint32_t kb = 0;
@@ -335,11 +333,10 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(7))
     }
     uint32_t tbn = TBS - 3 * (blockIdx.x & 3);
     const uint64_t availB = IN::bytes(avail);
-    const uint32_t vo = IN::voff((int)li);
+    const uint32_t vo1 = IN::voff(lane), vo2 = IN::voff((int)li);
     __amdgpu_buffer_rsrc_t rs = tg_rsrc<CH>(in, start, availB);
-    typename IN::raw_t rA = IN::template load<0>(rs, vo);
-    typename IN::raw_t rB = IN::template load<1>(rs, vo);
-    typename IN::raw_t rC = IN::template load<2>(rs, vo);
+    typename IN::raw_t rA = IN::template load<0>(rs, vo1);  // stage `lane` of the group
+    typename IN::raw_t rB = IN::template load<2>(rs, vo2);  // stage 64 + li
 
     // Branch-metric table reads, software-pipelined: the entries of stage r are loaded TGD stages
     // ahead; one ds_read_b64 at an even period also carries the entry of the stage 6 later.  The
@@ -458,24 +455,23 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(7))
             }
         }
     };
-    const int r6a = (int)li % 6, r6b = (int)(li + 32) % 6, r6c = (int)(li + 64) % 6;
+    const int r6a = lane % 6, r6b = (int)(li + 64) % 6;
     for (uint32_t j = 0;; j += 3) {
         // group head: the table from the inputs loaded one group ago, the next group's loads, then the
         // fairness board (its atomic returns during this group; nothing here waits on it)
-        if (lane < 32 && !(ABL & 8)) {  // ABL 8 (tools only): no table build
+        if constexpr (!(ABL & 8)) {  // ABL 8 (tools only): no table build
             int A, B;
-            IN::ab(rA, (int)li, A, B);
-            put_row(rowb[0], A, B, r6a);
-            IN::ab(rB, (int)li, A, B);
-            put_row(rowb[1], A, B, r6b);
-            IN::ab(rC, (int)li, A, B);
-            put_row(rowb[2], A, B, r6c);
+            IN::ab(rA, lane, A, B);
+            put_row(rowb1, A, B, r6a);
+            if (lane < 32) {
+                IN::ab(rB, (int)li, A, B);
+                put_row(rowb2, A, B, r6b);
+            }
         }
         if constexpr (!(ABL & 16)) {
             rs = tg_rsrc<CH>(in, start + 32ull * (j + 3), availB);
-            rA = IN::template load<0>(rs, vo);
-            rB = IN::template load<1>(rs, vo);
-            rC = IN::template load<2>(rs, vo);
+            rA = IN::template load<0>(rs, vo1);
+            rB = IN::template load<2>(rs, vo2);
         }
         if constexpr (!(ABL & 256)) {
             if (fb) {

@@ -85,6 +85,18 @@ def kstage(kind, P="v10", tab=False, nop_after=False):
     elif kind == "swapadd_nonop":
         o += [f"v_add_f32 v14, {P}, v40", f"v_add_f32 v18, {P}, v41",
               "v_permlane32_swap_b32 v14, v18", f"v_max_f32 {P}, v14, v18"]
+    elif kind == "swap_nop0":
+        o += [f"v_fma_f32 v14, v40, v41, {P}", f"v_fma_f32 v18, v40, -v41, {P}", "s_nop 0",
+              "v_permlane32_swap_b32 v14, v18", f"v_max_f32 {P}, v14, v18"]
+    elif kind == "swap_mov":
+        o += [f"v_mov_b32 v14, {P}", "s_nop 1", f"v_permlane32_swap_b32 v14, {P}",
+              "v_add_f32 v18, v14, v40", f"v_sub_f32 v14, {P}, v40", f"v_max_f32 {P}, v14, v18"]
+    elif kind == "swap_pk":
+        o += [f"v_pk_add_f32 v[14:15], v[{P[1:]}:{int(P[1:])+1}], v[40:41] op_sel_hi:[0,1]", "s_nop 1",
+              "v_permlane32_swap_b32 v14, v15", f"v_max_f32 {P}, v14, v15"]
+    elif kind == "swap_max_nop":
+        o += [f"v_fma_f32 v14, v40, v41, {P}", f"v_fma_f32 v18, v40, -v41, {P}", "s_nop 1",
+              "v_permlane32_swap_b32 v14, v18", "s_nop 0", f"v_max_f32 {P}, v14, v18"]
     elif kind == "bperm":
         o += [f"ds_bpermute_b32 v18, v43, {P}", f"v_add_f32 v14, {P}, v40", "s_waitcnt lgkmcnt(0)",
               "v_sub_f32 v18, v18, v40", f"v_max_f32 {P}, v14, v18"]
@@ -111,7 +123,9 @@ V += [("K dpp stage", seq(["dpp"], 24), 24), ("K dpp stage, no nop", seq(["dpp_n
       ("K swap stage (fma)", seq(["swapfma"], 24), 24), ("K swap stage (add)", seq(["swapadd"], 24), 24),
       ("K swap stage (add, no nop)", seq(["swapadd_nonop"], 24), 24), ("K bpermute stage", seq(["bperm"], 24), 24),
       ("K period 4dpp+2swap", seq(PERIOD, 4), 24), ("K period + nop after", seq(PERIOD, 4, nop_after=True), 24),
-      ("K period + tab read", seq(PERIOD, 4, tab=True), 24)]
+      ("K period + tab read", seq(PERIOD, 4, tab=True), 24),
+      ("K swap stage nop0", seq(["swap_nop0"], 24), 24), ("K swap stage mov", seq(["swap_mov"], 24), 24),
+      ("K swap stage pk_add", seq(["swap_pk"], 24, P="v12"), 24), ("K swap stage max-nop", seq(["swap_max_nop"], 24), 24)]
 CLB = ','.join(f'"v{i}"' for i in list(range(10, 26)) + [40, 41, 42, 43])
 src = ['// generated by tools/gen/gen_ubench10.py -- do not edit', '#include <hip/hip_runtime.h>', '#include <cstdio>',
        '#include <vector>', '#include <algorithm>',
