@@ -12,9 +12,10 @@
 // The history h = sum of the chosen signed digits (+-2^i, i < j) satisfies |h| < 2^j, so on equal
 // metrics the tag decides (the tie rule), and on unequal metrics (a difference of >= 2^S) neither tags
 // nor history can flip the order: every decision equals the reference's int32/int16/fp16 decision.
-// After J stages the field is read out -- r = round(V / 2^S) * 2^S via the 1.5*2^(23+S) magic add,
-// h = V - r -- and cleared (V = r).  The decision bits are (h + 2^J - 1) / 2, accumulated per 16 stages
-// into the low mantissa bits of 2^24 + (65535 + sum).
+// V is kept in [2^23, 2^24) (offset 1.5*2^23), where the fp32 ulp is 1 and the low mantissa bits are
+// the low integer bits, and each field starts at 2^(S-1): after J stages the field 2^(S-1) + h is in
+// (0, 2^S), its decision bits (h + 2^J - 1) / 2 are mantissa bits 1..J, and clearing it is one
+// v_and_or_b32.  Renormalising every 16 stages keeps |metric| < 2^(22-S).
 //
 // Lane encoding.  Position p (the trellis state rotr6(p, t%6) after stage t, as in vd_decode_sc) lives
 // in lane l = p0*1 ^ p1*2 ^ p2*7 ^ p3*8 ^ p4*16 ^ p5*32, so the butterfly partner p ^ (1<<q) is lane
@@ -33,8 +34,9 @@ struct TgFmt {
     static constexpr int J = CH == HARD ? 16 : 8;  // stages per history field
     static constexpr int S = J + 1;                // metric scale 2^S
 };
-// |metric| after the per-block renormalisation, bounded by (K-1)*(BMmax-BMmin) + 32*BMmax:
-//   HARD 12+32 = 44 < 2^(24-17);  SOFT4/FP32 192+512 = 704 < 2^15;  SOFT8 3072+8192 = 11264 < 2^15.
+// |metric| relative to position 0's at the last renormalisation (every 16 stages), bounded by
+// (K-1)*(BMmax-BMmin) + 16*BMmax, must stay below 2^(22-S) (V in [2^23, 2^24) with t1/t2 margins):
+//   HARD 12+16 = 28 < 32;  SOFT4/FP32 192+256 = 448 < 8192;  SOFT8 3072+4096 = 7168 < 8192.
 
 // branch-metric table: per 96-stage group, 16 periods of 6 rows (row K = stage phase); a row holds
 // BM[L]*2^S + c*2^j for the four labels L.  M_B32 rows of phase 0 hold a second set with the other
@@ -43,18 +45,19 @@ struct TgFmt {
 // entry e of row r sits at row(r) + 8e.
 template <int CORE>
 struct TgTab {
-    static constexpr int PB = CORE == B32 ? 112 : 96;  // bytes per 6-stage period
-    static __host__ __device__ constexpr int koff(int K) { return CORE == B32 ? (K == 0 ? 0 : 16 + 16 * K) : 16 * K; }
-    static __host__ __device__ constexpr int row(int r)
+    // dword offsets: period pair m at 60m, row K at KS[K] (8 dwords, M_B32's phase-0 row 16), padded so
+    // the 32-lane ds_write2_b32 of a table build hit (nearly) distinct banks (tools: bank search)
+    static __host__ __device__ constexpr int ks(int K)
     {
-        return (r / 12) * 2 * PB + 2 * koff(r % 6) + 4 * ((r / 6) % 2);
+        return CORE == B32 ? (K == 0 ? 0 : K == 1 ? 18 : K == 2 ? 26 : K == 3 ? 34 : K == 4 ? 44 : 52) : 10 * K;
     }
-    static constexpr int BYTES = 16 * PB;
+    static __host__ __device__ constexpr int row(int r) { return 4 * (60 * (r / 12) + ks(r % 6) + (r / 6) % 2); }
+    static constexpr int BYTES = 8 * 60 * 4;
 };
 // survivor ring slots per wave: table + ring of 4 waves fit 7 workgroups per CU (<= 22.8 KiB each)
 template <int CORE>
 struct TgRing {
-    static constexpr int TBS = CORE == B32 ? 13 : 14;
+    static constexpr int TBS = 13;
 };
 
 __device__ __forceinline__ int tg_pos(int l)
@@ -107,19 +110,6 @@ __device__ __forceinline__ void tg_stage_swap(float& V, float e1, float e2, floa
             "v_permlane32_swap_b32 %1, %2\n\tv_max_f32 %0, %1, %2"
             : "+v"(V), "=&v"(a), "=&v"(b) : "v"(e1), "v"(e2), "v"(sx));
 }
-// read out and clear the history field: r = round(V / 2^S) * 2^S, h = V - r
-template <int S>
-__device__ __forceinline__ void tg_cleanup(float V, float& r, float& h)
-{
-    static_assert(S == 9 || S == 17, "magic constant");
-    if constexpr (S == 9)  // 1.5 * 2^32
-        asm("v_add_f32 %0, 0x4fc00000, %2\n\tv_subrev_f32 %0, 0x4fc00000, %0\n\tv_sub_f32 %1, %2, %0"
-            : "=&v"(r), "=&v"(h) : "v"(V));
-    else  // 1.5 * 2^40
-        asm("v_add_f32 %0, 0x53c00000, %2\n\tv_subrev_f32 %0, 0x53c00000, %0\n\tv_sub_f32 %1, %2, %0"
-            : "=&v"(r), "=&v"(h) : "v"(V));
-}
-
 // ---------------------------------------------------------------- group traceback (reference viterbiTB.cuh:4-21)
 // Ring slot = 64 words indexed by position; byte/half g of word p holds the take-bits of history field
 // g along the survivor ending at p (register exchange within the field).  Tracing word k from state
@@ -277,8 +267,6 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(7))
     using TT = TgTab<CORE>;
     constexpr int J = TgFmt<CH>::J, S = TgFmt<CH>::S;
     constexpr int TBS = TgRing<CORE>::TBS;
-    // F16 (own wins ties everywhere) accumulates -h so the ring holds take-bits directly
-    constexpr float SG = CORE == F16 ? -1.0f : 1.0f;
     __shared__ __attribute__((aligned(16))) char tab_all[kWaves][TT::BYTES];
     __shared__ __attribute__((aligned(256))) uint32_t ring_all[kWaves][(TBS + 1) * 64];  // bit 31-s = stage s
     const int lane = threadIdx.x & 63;
@@ -320,7 +308,12 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(7))
     const float tg0 = CORE == F16 ? tagv : -tagv;  // tag of the row's own class
     const int rowb1 = TT::row(lane), rowb2 = TT::row(64 + (int)li);
 
-    float V = 0.0f;
+    // V lives in [2^23, 2^24), where the fp32 ulp is 1 and the low mantissa bits ARE the low integer
+    // bits: V = 1.5*2^23 + metric*2^S + 2^(S-1) + h.  The 2^(S-1) offset keeps the history field
+    // 2^(S-1) + h in (0, 2^S), so read-out and clearing are bit operations on the pattern.
+    constexpr uint32_t VBASE = 0x4B400000u + (1u << (S - 1));  // pattern of 1.5*2^23 + 2^(S-1)
+    float V = __builtin_bit_cast(float, VBASE);
+    const uint32_t fnm = ~((1u << S) - 1u), fhf = 1u << (S - 1);  // field clear: (p & fnm) | fhf
     uint32_t kb = 0;
     unsigned long long* fb = nullptr;
     unsigned long long fret = 0;
@@ -371,7 +364,7 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(7))
     auto block = [&](auto PHc, uint32_t j) {
         constexpr int PH = decltype(PHc)::value;
         constexpr int BB = PH / 2;
-        float acc = 0.0f, y0 = 0.0f, y1 = 0.0f;
+        uint32_t word = 0;
         sfor<32>([&](auto I) {
             constexpr int i = decltype(I)::value;
             constexpr int K = (PH + i) % 6;
@@ -389,23 +382,24 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(7))
             }
             if constexpr (r + TGD < 96) issue(std::integral_constant<int, r + TGD>{});
             if constexpr (i % J == J - 1 && !(ABL & 4)) {
-                float vr, h;
-                tg_cleanup<S>(V, vr, h);
-                V = vr;
-                if constexpr ((i % 16) / J == 0) acc = 65535.0f + SG * h;
-                else acc = __builtin_fmaf(h, SG * 256.0f, acc);
+                // field read-out: bits (2^(S-1) + h) >> 1 = (h + 2^J - 1) / 2, then clear to 2^(S-1)
+                uint32_t bits;
+                asm("v_bfe_u32 %1, %0, 1, %4\n\tv_and_or_b32 %0, %0, %2, %3"
+                    : "+v"(V), "=&v"(bits) : "v"(fnm), "v"(fhf), "n"(J));
+                constexpr int g = (i % 32) / J;
+                if constexpr (g == 0) word = bits;
+                else word |= bits << (J * g);
                 if constexpr (i % 16 == 15) {
-                    if constexpr (i < 16) y0 = acc + 16777216.0f;
-                    else y1 = acc + 16777216.0f;
+                    // decision-neutral renormalisation by the metric of position 0, every 16 stages
+                    const uint32_t p0 = __builtin_amdgcn_readfirstlane(__builtin_bit_cast(uint32_t, V));
+                    V = __builtin_bit_cast(float, __builtin_bit_cast(uint32_t, V) - (p0 - VBASE));
                 }
             }
         });
         // ring word of position p: byte (J=8) / half (J=16) g = the J path bits of the survivor that
-        // ends at p at the end of history field g of this block, stage 8g+j (16g+j) at bit j of it
-        const uint32_t word =
-            __builtin_amdgcn_perm(__builtin_bit_cast(uint32_t, y1), __builtin_bit_cast(uint32_t, y0), 0x05040100u);
-        // decision-neutral renormalisation by the metric of position 0 (V is a multiple of 2^S here)
-        V -= __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, V)));
+        // ends at p at the end of history field g of this block, stage 8g+j (16g+j) at bit j of it;
+        // the bits mark the tie-winning candidate, i.e. the take-bit except where the own one wins (F16)
+        if constexpr (CORE == F16) word = ~word;
         if constexpr (ABL & 64) ((uint32_t*)out + (1u << 20))[j * 64 + pos] = word;  // tools: ring words
         wave_sync();
         if (j >= 1) ring[(j - 1 - kb) * 64 + pos] = word;

@@ -82,11 +82,10 @@ def tg_model(AB, core, J):
     S = J + 1
     lanes = np.arange(64)
     pos = np.array([tg_pos(l) for l in lanes])
-    V = np.zeros(64, dtype=f32)
+    VBASE = np.uint32(0x4B400000 + (1 << (S - 1)))
+    V = np.full(64, VBASE, dtype=np.uint32).view(f32)
     takes = []
     nst = len(AB)
-    MG = f32(1.5 * 2.0 ** (23 + S))
-    SG = f32(-1.0) if core == "f16" else f32(1.0)
     acc = f32(0)
     hs = []
     for t in range(nst):
@@ -132,18 +131,19 @@ def tg_model(AB, core, J):
                     b2[l] = Y[l]
             V = np.maximum(a2, b2).astype(f32)
         if j == J - 1:
-            u = (V + MG).astype(f32)
-            r = (u - MG).astype(f32)
-            h = (V - r).astype(f32)
-            V = r
-            hs.append(h)
-        if t % 32 == 31:
-            V = (V - V[0]).astype(f32)
+            pat = V.view(np.uint32)
+            bits = ((pat >> 1) & ((1 << J) - 1)).astype(np.int64)
+            pat = (pat & np.uint32(~((1 << S) - 1) & 0xFFFFFFFF)) | np.uint32(1 << (S - 1))
+            if t % 16 == 15:
+                pat = (pat - (pat[0] - VBASE)).astype(np.uint32)
+            V = pat.view(f32)
+            if core == "f16":
+                bits = (~bits) & ((1 << J) - 1)
+            hs.append(bits)
+        assert np.all((V.view(np.uint32) >> 23) == 0x96), "left [2^23, 2^24)"
     # per group: the J path bits of the survivor ending at each position (lane -> position index)
     words = []
-    for h in hs:
-        hv = (SG * h).astype(np.float64)
-        bits = ((hv + (2 ** J - 1)) / 2).astype(np.int64)
+    for bits in hs:
         w = np.zeros(64, dtype=np.int64)
         w[pos] = bits
         words.append(w)
