@@ -45,13 +45,20 @@ struct TgFmt {
 // entry e of row r sits at row(r) + 8e.
 template <int CORE>
 struct TgTab {
-    // dword offsets: period pair m at 60m, row K at KS[K] (8 dwords, M_B32's phase-0 row 16), padded so
-    // the 32-lane ds_write2_b32 of a table build hit (nearly) distinct banks (tools: bank search)
+    // M_B32's phase-0 rows hold, per label and period, the pair (E-, E+) of both tag signs (its tie
+    // rule differs between the position halves there); every other row holds E[L] for the four labels
+    // with periods 2m, 2m+1 interleaved, so one ds_read_b64 serves a stage and the stage 6 later.
+    static __host__ __device__ constexpr bool pairrow(int K) { return CORE == B32 && K == 0; }
+    // dword offsets: period pair m at 60m, row K at ks(K) (8 dwords, M_B32's phase-0 row 16), padded so
+    // the 32-lane stores of a table build hit (nearly) distinct banks
     static __host__ __device__ constexpr int ks(int K)
     {
         return CORE == B32 ? (K == 0 ? 0 : K == 1 ? 18 : K == 2 ? 26 : K == 3 ? 34 : K == 4 ? 44 : 52) : 10 * K;
     }
-    static __host__ __device__ constexpr int row(int r) { return 4 * (60 * (r / 12) + ks(r % 6) + (r / 6) % 2); }
+    static __host__ __device__ constexpr int row(int r)
+    {
+        return 4 * (60 * (r / 12) + ks(r % 6) + ((r / 6) % 2) * (pairrow(r % 6) ? 8 : 1));
+    }
     static constexpr int BYTES = 8 * 60 * 4;
 };
 // survivor ring slots per wave: table + ring of 4 waves fit 7 workgroups per CU (<= 22.8 KiB each)
@@ -73,14 +80,21 @@ __device__ __forceinline__ int tg_cls(int p, int K)
     else if constexpr (CORE == B16) return 0;
     else return (K == 0 && (p & 32)) ? 1 : 0;
 }
-// float index of position p's own-transition entry within its phase-K row
-template <int CORE>
-__device__ __forceinline__ int tg_idx(int p, int K)
+// label flip of the butterfly partner in a swap stage: own_label(p ^ (1 << q), K) = own_label(p, K) ^ d
+__host__ __device__ constexpr int tg_par7(int v) { return (v & 1) ^ ((v >> 1) & 1) ^ ((v >> 2) & 1) ^ ((v >> 3) & 1) ^ ((v >> 4) & 1) ^ ((v >> 5) & 1) ^ ((v >> 6) & 1); }
+__host__ __device__ constexpr int tg_label(int p, int k)
 {
-    return ((CORE == B32 && K == 0) ? 4 * tg_cls<CORE>(p, K) : 0) + own_label(p, K);
+    const int T = ((p >> k) | (p << (6 - k))) & 63, r5 = (k + 5) % 6, O = ((p >> r5) | (p << (6 - r5))) & 63;
+    const int R = (T << 1) | (O & 1);
+    return (tg_par7(R & 0171) << 1) | tg_par7(R & 0133);
 }
+// label flip of the butterfly partner in the two swap phases: 0 (checked at compile time)
+static_assert(tg_label(32, 0) == 0 && tg_label(16, 5) == 0, "swap partners share the label");
 
 // ---------------------------------------------------------------- stages (inline asm, exact op order)
+// The path metric V is pinned to v60 ("{v60}" constraints) so that the swap stage's packed FMA can
+// name the pair v[60:61] and read V for both of its halves (op_sel_hi 0); v62:v63 are its scratch.
+typedef float f2v __attribute__((ext_vector_type(2)));
 // DPP stage, exchange lane xor {1,2,7,8}[Q].  The DPP source (V) is >= 2 VALU slots after its write.
 template <int Q>
 __device__ __forceinline__ void tg_stage_dpp(float& V, float m)
@@ -89,27 +103,34 @@ __device__ __forceinline__ void tg_stage_dpp(float& V, float m)
 #define VD_TG_DPP(CTRL)                                                                                   \
     asm("v_add_f32 %1, %0, %3\n\ts_nop 0\n\tv_sub_f32_dpp %2, %0, %3 " CTRL " row_mask:0xf bank_mask:0xf\n\t" \
         "v_max_f32 %0, %1, %2"                                                                           \
-        : "+v"(V), "=&v"(t1), "=&v"(t2) : "v"(m))
+        : "+{v60}"(V), "=&v"(t1), "=&v"(t2) : "v"(m))
     if constexpr (Q == 0) VD_TG_DPP("quad_perm:[1,0,3,2]");
     else if constexpr (Q == 1) VD_TG_DPP("quad_perm:[2,3,0,1]");
     else if constexpr (Q == 2) VD_TG_DPP("row_half_mirror");
     else VD_TG_DPP("row_ror:8");
 #undef VD_TG_DPP
 }
-// swap stage, exchange lane xor 16 (Q=4) or 32 (Q=5): a = V + sx*e1, b = V - sx*e2, swap halves, max
-template <int Q>
-__device__ __forceinline__ void tg_stage_swap(float& V, float e1, float e2, float sx)
+// swap stage, exchange lane xor 16 (Q=4) or 32 (Q=5): [a, b] = [m, m'] * [sx, -sx] + [V, V] in one
+// v_pk_fma_f32, swap halves across lanes, max.  The butterfly partner has the same label in both swap
+// phases, so m' = m except in M_B32's phase-0 rows (m, m' = the two tag signs).  SEL picks the halves of
+// the table pair e: 0 = (lo, lo) (even period), 1 = (hi, hi) (odd period), 2 = (lo, hi) (M_B32 phase 0).
+template <int Q, int SEL>
+__device__ __forceinline__ void tg_stage_swap(float& V, f2v e, f2v s)
 {
-    float a, b;
-    if constexpr (Q == 4)
-        asm("v_fma_f32 %1, %3, %5, %0\n\tv_fma_f32 %2, %4, -%5, %0\n\ts_nop 1\n\t"
-            "v_permlane16_swap_b32 %1, %2\n\tv_max_f32 %0, %1, %2"
-            : "+v"(V), "=&v"(a), "=&v"(b) : "v"(e1), "v"(e2), "v"(sx));
-    else
-        asm("v_fma_f32 %1, %3, %5, %0\n\tv_fma_f32 %2, %4, -%5, %0\n\ts_nop 1\n\t"
-            "v_permlane32_swap_b32 %1, %2\n\tv_max_f32 %0, %1, %2"
-            : "+v"(V), "=&v"(a), "=&v"(b) : "v"(e1), "v"(e2), "v"(sx));
+#define VD_TG_SWAP(SW, OS)                                                                            \
+    asm("v_pk_fma_f32 v[62:63], %1, %2, v[60:61] " OS "\n\ts_nop 1\n\t" SW " v62, v63\n\t"             \
+        "v_max_f32 %0, v62, v63"                                                                      \
+        : "+{v60}"(V) : "v"(e), "v"(s) : "v62", "v63")
+#define VD_TG_SWAP_SEL(SW)                                                                            \
+    if constexpr (SEL == 0) VD_TG_SWAP(SW, "op_sel:[0,0,0] op_sel_hi:[0,1,0]");                      \
+    else if constexpr (SEL == 1) VD_TG_SWAP(SW, "op_sel:[1,0,0] op_sel_hi:[1,1,0]");                 \
+    else VD_TG_SWAP(SW, "op_sel:[0,0,0] op_sel_hi:[1,1,0]");
+    if constexpr (Q == 4) { VD_TG_SWAP_SEL("v_permlane16_swap_b32") }
+    else { VD_TG_SWAP_SEL("v_permlane32_swap_b32") }
+#undef VD_TG_SWAP_SEL
+#undef VD_TG_SWAP
 }
+
 // ---------------------------------------------------------------- group traceback (reference viterbiTB.cuh:4-21)
 // Ring slot = 64 words indexed by position; byte/half g of word p holds the take-bits of history field
 // g along the survivor ending at p (register exchange within the field).  Tracing word k from state
@@ -283,24 +304,19 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(7))
     const uint32_t nblk = Sw + 2;
 
     // per-lane LDS byte addresses of this position's table entries (row offsets are compile-time)
-    int aD[4];
-    sfor<4>([&](auto KK) {
-        constexpr int K = decltype(KK)::value + 1;
-        aD[K - 1] = 8 * tg_idx<CORE>(pos, K);
+    // per-lane LDS byte offset of this position's entry in a phase-K row (row offsets are compile-time);
+    // [sx, -sx] route the swap stages' candidates (see tg_stage_swap and the file header)
+    int aK[6];
+    sfor<6>([&](auto KK) {
+        constexpr int K = decltype(KK)::value;
+        aK[K] = 8 * own_label(pos, K);
     });
-    int a1[2], a2[2];
-    float sx[2];
+    f2v sxp[2];
     sfor<2>([&](auto W) {
         constexpr int w = decltype(W)::value;  // 0: K=0 (Q=5), 1: K=5 (Q=4)
-        constexpr int K = w == 0 ? 0 : 5, Q = w == 0 ? 5 : 4;
-        const int pp = pos ^ (1 << Q), bit = (pos >> Q) & 1;
-        const int io = tg_idx<CORE>(pos, K), ix = tg_idx<CORE>(pp, K);
-        a1[w] = 8 * (bit ? ix : io);
-        a2[w] = 8 * (bit ? io : ix);
-        sx[w] = bit ? -1.0f : 1.0f;
+        constexpr int Q = w == 0 ? 5 : 4;
+        sxp[w] = ((pos >> Q) & 1) ? (f2v){-1.0f, 1.0f} : (f2v){1.0f, -1.0f};
     });
-    // table-build role: lane li writes rows li, 32+li, 64+li of each group
-    const uint64_t avail = geo.availStages;
     // table-build roles: every lane writes row `lane` (stages 0..63 of the group), lanes 0..31 also
     // row 64 + lane; J divides 32, so the tag position (row % J) is lane % J for both
     const uint64_t li = (uint64_t)(lane & 31);
@@ -325,7 +341,7 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(7))
         }
     }
     uint32_t tbn = TBS - 3 * (blockIdx.x & 3);
-    const uint64_t availB = IN::bytes(avail);
+    const uint64_t availB = IN::bytes(geo.availStages);
     const uint32_t vo1 = IN::voff(lane), vo2 = IN::voff((int)li);
     __amdgpu_buffer_rsrc_t rs = tg_rsrc<CH>(in, start, availB);
     typename IN::raw_t rA = IN::template load<0>(rs, vo1);  // stage `lane` of the group
@@ -336,29 +352,15 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(7))
     // loads are volatile LDS-address-space loads so they stay single ds_read_b64s (2 LDS cycles) in
     // program order -- left alone the compiler merges neighbours into ds_read2_b64 (8 cycles).
     constexpr int TGD = 4;
-    typedef float f2v __attribute__((ext_vector_type(2)));
     typedef __attribute__((address_space(3))) const volatile f2v* lptr;
     const __attribute__((address_space(3))) char* tl = (const __attribute__((address_space(3))) char*)tabb;
-    float va[96], vb[96];
+    f2v vp[96];  // entry pair read for stage r (even period of a pair, or every M_B32 phase-0 stage)
     auto issue = [&](auto Rc) {
         constexpr int r = decltype(Rc)::value;  // stage within the group (the group starts at phase 0)
-        if constexpr ((r / 6) % 2 == 0 && !(ABL & 2)) {
-            constexpr int K = r % 6;
-            constexpr int Q = (K + 5) % 6;
-            constexpr int ROWE = TT::row(r);
-            if constexpr (Q <= 3 || (ABL & 128)) {
-                const f2v v = *(lptr)(tl + aD[(K + 3) % 4] + ROWE);
-                va[r] = v.x;
-                va[r + 6] = v.y;
-            } else {
-                constexpr int w = K == 0 ? 0 : 1;
-                const f2v v1 = *(lptr)(tl + a1[w] + ROWE);
-                const f2v v2 = *(lptr)(tl + a2[w] + ROWE);
-                va[r] = v1.x;
-                va[r + 6] = v1.y;
-                vb[r] = v2.x;
-                vb[r + 6] = v2.y;
-            }
+        constexpr int K = r % 6;
+        if constexpr (ABL & 2) {
+        } else if constexpr (TT::pairrow(K) || (r / 6) % 2 == 0) {
+            vp[r] = *(lptr)(tl + aK[K] + TT::row(r));
         }
     };
     auto block = [&](auto PHc, uint32_t j) {
@@ -371,21 +373,21 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(7))
             constexpr int Q = (K + 5) % 6;
             constexpr int r = 32 * BB + i;  // stage within the group
             // ABL (tools only): 2 = no table reads, 128 = every stage a DPP stage, 4 = no field read-out
+            constexpr bool ODD = (r / 6) % 2 == 1;
+            constexpr int RP = TT::pairrow(K) ? r : (ODD ? r - 6 : r);  // where this stage's pair was read
             if constexpr (Q <= 3 || (ABL & 128)) {
-                const float m = (ABL & 2) ? (float)aD[(K + 3) % 4] : va[r];
+                const float m = (ABL & 2) ? (float)aK[K] : (ODD ? vp[RP].y : vp[RP].x);
                 tg_stage_dpp<(Q <= 3 ? Q : 3)>(V, m);
             } else {
-                constexpr int w = K == 0 ? 0 : 1;
-                const float e1 = (ABL & 2) ? (float)a1[w] : va[r];
-                const float e2 = (ABL & 2) ? (float)a2[w] : vb[r];
-                tg_stage_swap<Q>(V, e1, e2, sx[w]);
+                const f2v e = (ABL & 2) ? (f2v){(float)aK[K], 1.0f} : vp[RP];
+                tg_stage_swap<Q, TT::pairrow(K) ? 2 : (ODD ? 1 : 0)>(V, e, sxp[K == 0 ? 0 : 1]);
             }
             if constexpr (r + TGD < 96) issue(std::integral_constant<int, r + TGD>{});
             if constexpr (i % J == J - 1 && !(ABL & 4)) {
                 // field read-out: bits (2^(S-1) + h) >> 1 = (h + 2^J - 1) / 2, then clear to 2^(S-1)
                 uint32_t bits;
                 asm("v_bfe_u32 %1, %0, 1, %4\n\tv_and_or_b32 %0, %0, %2, %3"
-                    : "+v"(V), "=&v"(bits) : "v"(fnm), "v"(fhf), "n"(J));
+                    : "+{v60}"(V), "=&v"(bits) : "v"(fnm), "v"(fhf), "n"(J));
                 constexpr int g = (i % 32) / J;
                 if constexpr (g == 0) word = bits;
                 else word |= bits << (J * g);
@@ -426,26 +428,28 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(7))
         return j + 1 < nblk;
     };
     // one 96-stage group's table row from the stage's (A, B) = (BM[3], BM[2])
-    auto put_row = [&](int rb, int A, int B, int r6) {
+    // table row of stage phase K: E[L] = BM[L]*2^S + tag at entries 0, 2, 4, 6 (the odd dwords are the
+    // other period's); M_B32 phase-0 rows: the pairs (E-[L], E+[L]) of both tag signs
+    auto put_row = [&](int rb, int A, int B, int K) {
         constexpr float SC = (float)(1 << S);
         const float af = (float)A, bf = (float)B;
         float* e = (float*)(tabb + rb);
+        const float E0 = __builtin_fmaf(af, -SC, tg0), E1 = __builtin_fmaf(bf, -SC, tg0);
+        const float E2 = __builtin_fmaf(bf, SC, tg0), E3 = __builtin_fmaf(af, SC, tg0);
         if constexpr (ABL & 512) {  // tools only: compute the row, do not store it
-            float x0 = __builtin_fmaf(af, -SC, tg0), x1 = __builtin_fmaf(bf, -SC, tg0);
-            float x2 = __builtin_fmaf(bf, SC, tg0), x3 = __builtin_fmaf(af, SC, tg0);
-            asm volatile("" ::"v"(x0), "v"(x1), "v"(x2), "v"(x3));
+            asm volatile("" ::"v"(E0), "v"(E1), "v"(E2), "v"(E3));
             return;
         }
-        e[0] = __builtin_fmaf(af, -SC, tg0);
-        e[2] = __builtin_fmaf(bf, -SC, tg0);
-        e[4] = __builtin_fmaf(bf, SC, tg0);
-        e[6] = __builtin_fmaf(af, SC, tg0);
+        e[0] = E0;
+        e[2] = E1;
+        e[4] = E2;
+        e[6] = E3;
         if constexpr (CORE == B32) {
-            if (r6 == 0) {  // phase-0 row: the own-wins set (+tag) for the upper position half
-                e[8] = __builtin_fmaf(af, -SC, tagv);
-                e[10] = __builtin_fmaf(bf, -SC, tagv);
-                e[12] = __builtin_fmaf(bf, SC, tagv);
-                e[14] = __builtin_fmaf(af, SC, tagv);
+            if (K == 0) {
+                e[1] = __builtin_fmaf(af, -SC, tagv);
+                e[3] = __builtin_fmaf(bf, -SC, tagv);
+                e[5] = __builtin_fmaf(bf, SC, tagv);
+                e[7] = __builtin_fmaf(af, SC, tagv);
             }
         }
     };
