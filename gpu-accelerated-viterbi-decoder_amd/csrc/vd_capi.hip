@@ -18,6 +18,7 @@
 #include "../../include/vd_capi.h"
 #include "vd_kernels.h"
 #include "vd_kernel_tg.h"
+#include "vd_pack.h"
 #include "vd_synth.h"
 
 namespace {
@@ -123,6 +124,31 @@ launch_fn pick(int o)
     return nullptr;
 }
 
+// fused LLR decode: float channel values quantised in the table build (channel ids kLlr + base)
+template <int CH, int CORE, int OB>
+void launch_llr_t(const void* in, void* out, vd::Geom g, hipStream_t s)
+{
+    hipLaunchKernelGGL((vd::vd_decode_tg<vd::kLlr + CH, CORE, OB>), dim3((g.nchunks + vd::kWaves - 1) / vd::kWaves),
+                       dim3(64 * vd::kWaves), 0, s, in, out, g);
+}
+template <int CH, int CORE>
+launch_fn pick_llr_ob(int ob)
+{
+    return ob == 1 ? &launch_llr_t<CH, CORE, 16> : &launch_llr_t<CH, CORE, 32>;
+}
+// null for SOFT16 (its metrics need the untagged kernel: pack first, then decode)
+launch_fn pick_llr(int o)
+{
+    const int ch = ch_of(o), me = met_of(o), ob = out_of(o);
+    switch (ch) {
+    case 0: return me == 0 ? pick_llr_ob<0, 0>(ob) : me == 1 ? pick_llr_ob<0, 1>(ob) : pick_llr_ob<0, 2>(ob);
+    case 1: return me == 0 ? pick_llr_ob<1, 0>(ob) : me == 1 ? pick_llr_ob<1, 1>(ob) : pick_llr_ob<1, 2>(ob);
+    case 2: return me == 0 ? pick_llr_ob<2, 0>(ob) : pick_llr_ob<2, 1>(ob);
+    case 4: return me == 0 ? pick_llr_ob<4, 0>(ob) : me == 1 ? pick_llr_ob<4, 1>(ob) : pick_llr_ob<4, 2>(ob);
+    }
+    return nullptr;
+}
+
 const char* kname(int o)
 {
     static const char* names[5][3] = {
@@ -143,7 +169,8 @@ struct vd_decoder {
     int device = 0;
     void* in_d = nullptr;
     void* out_d = nullptr;
-    size_t cap_in = 0, cap_out = 0;
+    void* llr_d = nullptr;  // vd_run_llr's float input buffer
+    size_t cap_in = 0, cap_out = 0, cap_llr = 0;
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
 };
@@ -189,15 +216,18 @@ static unsigned long long* fair_board(int device)
     return boards[device];
 }
 
-static int launch_decode(int options, const void* in_d, void* out_d, size_t inputNum, hipStream_t s)
+// llr: in_d holds inputNum float channel values, quantised in the kernel (scale = packer scale)
+static int launch_decode(int options, const void* in_d, void* out_d, size_t inputNum, hipStream_t s,
+                         bool llr = false, float scale = 1.0f)
 {
-    launch_fn f = pick(options);
+    launch_fn f = llr ? pick_llr(options) : pick(options);
     if (!f) return fail(VD_ERR_OPTIONS, "invalid options");
     size_t msg = message_len(options, inputNum);
     vd::Geom g;
     g.packNum = msg / (size_t)bpp_of(options);
-    g.availStages = avail_stages(options, inputNum);
+    g.availStages = llr ? inputNum / 2 : avail_stages(options, inputNum);
     g.nchunks = vd::kChunks;
+    g.scale = scale;
     if (g.packNum == 0) return VD_OK;
     int dev = 0;
     VD_HIP(hipGetDevice(&dev));
@@ -257,6 +287,7 @@ int vd_destroy(vd_decoder* d)
     (void)hipSetDevice(d->device);
     if (d->in_d) (void)hipFree(d->in_d);
     if (d->out_d) (void)hipFree(d->out_d);
+    if (d->llr_d) (void)hipFree(d->llr_d);
     if (d->ev0) (void)hipEventDestroy(d->ev0);
     if (d->ev1) (void)hipEventDestroy(d->ev1);
     if (d->stream) (void)hipStreamDestroy(d->stream);
@@ -288,6 +319,74 @@ int vd_run_device(vd_decoder* d, const void* input_d, void* output_d, size_t inp
     if (!d || !input_d || !output_d) return fail(VD_ERR_ARG, "null argument");
     if (message_len(d->options, inputNum) == 0) return fail(VD_ERR_ARG, "inputNum too small");
     return launch_decode(d->options, input_d, output_d, inputNum, (hipStream_t)stream);
+}
+
+static int launch_pack(int options, const float* llr_d, size_t inputNum, float scale, void* packed_d, hipStream_t s)
+{
+    if (((uintptr_t)llr_d & 15) != 0) return fail(VD_ERR_ARG, "llr buffer must be 16-byte aligned");
+    const int ch = ch_of(options);
+    const int per = ch == 0 ? 32 : ch == 1 ? 8 : ch == 2 ? 4 : ch == 3 ? 2 : 1;
+    const uint64_t nw = (inputNum + per - 1) / per;
+    if (nw == 0) return VD_OK;
+    const dim3 blk(256), grd((unsigned)((nw + 255) / 256));
+    switch (ch) {
+    case 0: hipLaunchKernelGGL(vd::pack_llr<0>, grd, blk, 0, s, llr_d, (uint64_t)inputNum, scale, packed_d); break;
+    case 1: hipLaunchKernelGGL(vd::pack_llr<1>, grd, blk, 0, s, llr_d, (uint64_t)inputNum, scale, packed_d); break;
+    case 2: hipLaunchKernelGGL(vd::pack_llr<2>, grd, blk, 0, s, llr_d, (uint64_t)inputNum, scale, packed_d); break;
+    case 3: hipLaunchKernelGGL(vd::pack_llr<3>, grd, blk, 0, s, llr_d, (uint64_t)inputNum, scale, packed_d); break;
+    case 4: hipLaunchKernelGGL(vd::pack_llr<4>, grd, blk, 0, s, llr_d, (uint64_t)inputNum, scale, packed_d); break;
+    }
+    VD_HIP(hipGetLastError());
+    return VD_OK;
+}
+
+int vd_pack_device(int options, const float* llr_d, size_t inputNum, float scale, void* packed_d, void* stream)
+{
+    if (!valid(options)) return fail(VD_ERR_OPTIONS, "options disabled by OptionsValid");
+    if (!llr_d || !packed_d) return fail(VD_ERR_ARG, "null argument");
+    return launch_pack(options, llr_d, inputNum, scale, packed_d, (hipStream_t)stream);
+}
+
+int vd_run_device_llr(vd_decoder* d, const float* llr_d, void* output_d, size_t inputNum, float scale, void* stream)
+{
+    if (!d || !llr_d || !output_d) return fail(VD_ERR_ARG, "null argument");
+    if (message_len(d->options, inputNum) == 0) return fail(VD_ERR_ARG, "inputNum too small");
+    hipStream_t s = (hipStream_t)stream;
+    if (ch_of(d->options) == 3) {  // SOFT16: pack into the decoder's buffer, then the untagged decode
+        VD_HIP(hipSetDevice(d->device));
+        int rc = ensure_capacity(d, input_size(d->options, inputNum), 0);
+        if (rc != VD_OK) return rc;
+        rc = launch_pack(d->options, llr_d, inputNum, scale, d->in_d, s);
+        if (rc != VD_OK) return rc;
+        return launch_decode(d->options, d->in_d, output_d, inputNum, s);
+    }
+    return launch_decode(d->options, llr_d, output_d, inputNum, s, true, scale);
+}
+
+int vd_run_llr(vd_decoder* d, const float* llr_h, void* output_h, size_t inputNum, float scale, float* kernel_ms)
+{
+    if (!d || !llr_h || !output_h) return fail(VD_ERR_ARG, "null argument");
+    if (message_len(d->options, inputNum) == 0) return fail(VD_ERR_ARG, "inputNum too small");
+    const size_t inB = inputNum * sizeof(float), outB = message_len(d->options, inputNum) / 8;
+    VD_HIP(hipSetDevice(d->device));
+    if (inB > d->cap_llr) {
+        if (d->llr_d) (void)hipFree(d->llr_d);
+        d->llr_d = nullptr;
+        d->cap_llr = 0;
+        VD_HIP(hipMalloc(&d->llr_d, inB));
+        d->cap_llr = inB;
+    }
+    int rc = ensure_capacity(d, ch_of(d->options) == 3 ? input_size(d->options, inputNum) : 0, outB + 16);
+    if (rc != VD_OK) return rc;
+    VD_HIP(hipMemcpyAsync(d->llr_d, llr_h, inB, hipMemcpyHostToDevice, d->stream));
+    VD_HIP(hipEventRecord(d->ev0, d->stream));
+    rc = vd_run_device_llr(d, (const float*)d->llr_d, d->out_d, inputNum, scale, d->stream);
+    if (rc != VD_OK) return rc;
+    VD_HIP(hipEventRecord(d->ev1, d->stream));
+    VD_HIP(hipMemcpyAsync(output_h, d->out_d, outB, hipMemcpyDeviceToHost, d->stream));
+    VD_HIP(hipStreamSynchronize(d->stream));
+    if (kernel_ms) VD_HIP(hipEventElapsedTime(kernel_ms, d->ev0, d->ev1));
+    return VD_OK;
 }
 
 int vd_run_batches(int options, const void* const* input_h, void* const* output_h, size_t inputNum,

@@ -25,13 +25,17 @@
 // its exchanged candidate (X, Y = +-M of the lane and of its partner, from the branch-metric table).
 #pragma once
 #include "vd_kernels.h"
+#include "vd_pack.h"
 
 namespace vd {
 
+// channel ids: HARD..FP32 = packed input (viterbiBM.cuh formats); 8 + base = float channel values
+// quantised on the fly exactly like SoftDecisionPacker(base, scale) would have packed them (vd_pack.h)
+constexpr int kLlr = 8;
 template <int CH>
 struct TgFmt {
-    static_assert(CH != SOFT16, "SOFT16 metrics do not leave room for decision tags");
-    static constexpr int J = CH == HARD ? 16 : 8;  // stages per history field
+    static_assert((CH & 7) != SOFT16, "SOFT16 metrics do not leave room for decision tags");
+    static constexpr int J = (CH & 7) == HARD ? 16 : 8;  // stages per history field
     static constexpr int S = J + 1;                // metric scale 2^S
 };
 // |metric| relative to position 0's at the last renormalisation (every 16 stages), bounded by
@@ -205,7 +209,7 @@ struct TgIn<HARD> {  // 16 stages per word; stage g -> bits 31-2(g%16), 30-2(g%1
     {
         return __builtin_amdgcn_raw_buffer_load_b32(rs, vo + R * RB, 0, 0);
     }
-    static __device__ __forceinline__ void ab(raw_t w, int li, int& A, int& B)
+    static __device__ __forceinline__ void ab(raw_t w, int li, int& A, int& B, float)
     {
         const int sh = 30 - 2 * (li & 15);
         const int r0 = (w >> (sh + 1)) & 1, r1 = (w >> sh) & 1;
@@ -224,7 +228,7 @@ struct TgIn<SOFT4> {  // 4 stages per word, byte g%4 from the MSB: high nibble s
     {
         return __builtin_amdgcn_raw_buffer_load_b32(rs, vo + R * RB, 0, 0);
     }
-    static __device__ __forceinline__ void ab(raw_t w, int li, int& A, int& B)
+    static __device__ __forceinline__ void ab(raw_t w, int li, int& A, int& B, float)
     {
         const int sh = 24 - 8 * (li & 3);
         const int s0 = (int)(w << (24 - sh)) >> 28, s1 = (int)(w << (28 - sh)) >> 28;
@@ -243,7 +247,7 @@ struct TgIn<SOFT8> {  // 2 stages per word; the 16-bit half g^1 holds s0 (high b
     {
         return (uint32_t)__builtin_amdgcn_raw_buffer_load_b16(rs, vo + R * RB, 0, 0);
     }
-    static __device__ __forceinline__ void ab(raw_t w, int, int& A, int& B)
+    static __device__ __forceinline__ void ab(raw_t w, int, int& A, int& B, float)
     {
         const int s0 = (int)(w << 16) >> 24, s1 = (int)(w << 24) >> 24;
         A = s0 + s1;
@@ -263,13 +267,46 @@ struct TgIn<FP32> {  // 2 floats per stage, clamped to [-8,7]; BM = (int)(+-x0 +
         const f2 v = __builtin_bit_cast(f2, __builtin_amdgcn_raw_buffer_load_b64(rs, vo + R * RB, 0, 0));
         return make_float2(v.x, v.y);
     }
-    static __device__ __forceinline__ void ab(raw_t v, int, int& A, int& B)
+    static __device__ __forceinline__ void ab(raw_t v, int, int& A, int& B, float)
     {
         const float x0 = fminf(fmaxf(v.x, -8.0f), 7.0f), x1 = fminf(fmaxf(v.y, -8.0f), 7.0f);
         A = (int)__fadd_rn(x0, x1);
         B = (int)__fsub_rn(x0, x1);
     }
 };
+// float channel values (2 per stage, 8 bytes), quantised as SoftDecisionPacker(BASE, scale) would
+template <int BASE>
+struct TgInLlr {
+    using raw_t = float2;
+    static constexpr int RB = 256;
+    static __device__ __forceinline__ uint64_t bytes(uint64_t stages) { return stages * 8; }
+    static __device__ __forceinline__ uint32_t voff(int li) { return 8u * (uint32_t)li; }
+    template <int R>
+    static __device__ __forceinline__ raw_t load(__amdgpu_buffer_rsrc_t rs, uint32_t vo)
+    {
+        return TgIn<FP32>::template load<R>(rs, vo);
+    }
+    static __device__ __forceinline__ void ab(raw_t v, int li, int& A, int& B, float scale)
+    {
+        if constexpr (BASE == FP32) {
+            TgIn<FP32>::ab(make_float2(v.x * scale, v.y * scale), li, A, B, scale);
+        } else {
+            const int s0 = code_value<BASE>(pack_code<BASE>(v.x * scale));
+            const int s1 = code_value<BASE>(pack_code<BASE>(v.y * scale));
+            if constexpr (BASE == HARD) {
+                A = s0 + s1 - 1;  // 1 - #mismatches against (1,1)
+                B = s0 - s1;      // against (1,0)
+            } else {
+                A = s0 + s1;
+                B = s0 - s1;
+            }
+        }
+    }
+};
+template <> struct TgIn<kLlr + HARD> : TgInLlr<HARD> {};
+template <> struct TgIn<kLlr + SOFT4> : TgInLlr<SOFT4> {};
+template <> struct TgIn<kLlr + SOFT8> : TgInLlr<SOFT8> {};
+template <> struct TgIn<kLlr + FP32> : TgInLlr<FP32> {};
 // resource for the 96 stages from g0 (g0 a multiple of 16; inputs below 4 GiB)
 template <int CH>
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t tg_rsrc(const void* in, uint64_t g0, uint64_t availBytes)
@@ -459,10 +496,10 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(7))
         // fairness board (its atomic returns during this group; nothing here waits on it)
         if constexpr (!(ABL & 8)) {  // ABL 8 (tools only): no table build
             int A, B;
-            IN::ab(rA, lane, A, B);
+            IN::ab(rA, lane, A, B, geo.scale);
             put_row(rowb1, A, B, r6a);
             if (lane < 32) {
-                IN::ab(rB, (int)li, A, B);
+                IN::ab(rB, (int)li, A, B, geo.scale);
                 put_row(rowb2, A, B, r6b);
             }
         }

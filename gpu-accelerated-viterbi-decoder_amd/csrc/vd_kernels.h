@@ -43,6 +43,7 @@ struct Geom {
     uint64_t availStages;  // stages readable from the input buffer
     uint32_t nchunks;
     unsigned long long* fair;  // per-SIMD progress board (kFairSlots words, zero at rest) or null
+    float scale;               // LLR input (channel ids 8 + base): SoftDecisionPacker scale, else unused
 };
 // progress board: one 64-bit word per SIMD slot, (waves << 32) + blocks started; indexed by
 // (XCC, SE, SH, CU, SIMD) from the hardware wave id.  Only issue priority depends on it.

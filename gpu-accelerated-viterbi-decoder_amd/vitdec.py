@@ -40,7 +40,8 @@ _ERRNAMES = {-1: "VD_ERR_OPTIONS", -2: "VD_ERR_ARG", -3: "VD_ERR_DEVICE", -4: "V
 # every entry point declared in include/vd_capi.h (tests check the library exports all of them)
 EXPORTS = ["vd_options_valid", "vd_input_size", "vd_message_len", "vd_output_size", "vd_num_chunks",
            "vd_create", "vd_destroy", "vd_run", "vd_run_device", "vd_run_batches", "vd_synth_device",
-           "vd_simulate_host", "vd_count_errors", "vd_last_error", "vd_device_count", "vd_kernel_name"]
+           "vd_simulate_host", "vd_count_errors", "vd_last_error", "vd_device_count", "vd_kernel_name",
+           "vd_pack_device", "vd_run_device_llr", "vd_run_llr"]
 
 
 class VitdecError(RuntimeError):
@@ -74,6 +75,9 @@ def lib():
     L.vd_count_errors.argtypes = [i, vp, sz, vp, sz]
     L.vd_count_errors.restype = ctypes.c_longlong
     L.vd_last_error.restype = ctypes.c_char_p
+    L.vd_pack_device.argtypes = [i, vp, sz, f, vp, vp]
+    L.vd_run_device_llr.argtypes = [vp, vp, vp, sz, f, vp]
+    L.vd_run_llr.argtypes = [vp, vp, vp, sz, f, ctypes.POINTER(f)]
     L.vd_kernel_name.argtypes = [i]
     L.vd_kernel_name.restype = ctypes.c_char_p
     _lib = L
@@ -185,6 +189,30 @@ class ViterbiCUDA:
         """Async device decode: raw device pointers on self.device, HIP stream handle (int)."""
         _check(lib().vd_run_device(self._h, ctypes.c_void_p(input_ptr), ctypes.c_void_p(output_ptr), inputNum,
                                    ctypes.c_void_p(stream)))
+
+
+    # ---- float channel values (SoftDecisionPacker(channel, scale) fused into the decode) ----
+    def run_llr(self, llr_h, scale=40000.0, output_h=None):
+        """Blocking decode of float channel values (viterbiDF.h:98-167 packer fused). Returns (out, ms)."""
+        llr_h = np.ascontiguousarray(llr_h, dtype=np.float32)
+        inputNum = llr_h.size
+        if output_h is None:
+            output_h = np.zeros(self.getOutputSize(inputNum) // np.dtype(self.decPack_t).itemsize,
+                                dtype=self.decPack_t)
+        ms = ctypes.c_float(0.0)
+        _check(lib().vd_run_llr(self._h, llr_h.ctypes.data, output_h.ctypes.data, inputNum, scale, ctypes.byref(ms)))
+        return output_h, ms.value
+
+    def run_device_llr(self, llr_ptr, output_ptr, inputNum, scale=40000.0, stream=0):
+        """Async fused decode of inputNum device floats (16-byte aligned)."""
+        _check(lib().vd_run_device_llr(self._h, ctypes.c_void_p(llr_ptr), ctypes.c_void_p(output_ptr), inputNum,
+                                       scale, ctypes.c_void_p(stream)))
+
+
+def pack_device(options, llr_ptr, inputNum, packed_ptr, scale=40000.0, stream=0):
+    """The reference's SoftDecisionPacker on device floats -> vd_input_size(options, inputNum) bytes."""
+    _check(lib().vd_pack_device(options, ctypes.c_void_p(llr_ptr), inputNum, scale, ctypes.c_void_p(packed_ptr),
+                                ctypes.c_void_p(stream)))
 
 
 def synth_device(options, n_bits, snr, seed, bits_ptr, packed_ptr, stream=0):

@@ -80,6 +80,23 @@ int vd_run_device(vd_decoder* dec, const void* input_d, void* output_d, size_t i
 int vd_run_batches(int options, const void* const* input_h, void* const* output_h, size_t inputNum,
                    int nbatches, const int* devices, int ndev, float* wall_ms);
 
+/* ---- float channel values (the reference's SoftDecisionPacker stage, viterbiDF.h:98-167) ----
+ * The reference packs float channel values on the host (quant(v*scale): HARD v > 0; SOFT4/SOFT8
+ * (int)lrintf saturated to 4/8 bits; SOFT16 lrintf saturated to 16 bits; FP32 v*scale; MSB-first
+ * words) and copies the packed words to the GPU.  These entry points take the floats on the device
+ * instead; results are bit-identical to packing with SoftDecisionPacker(channel, scale) and then
+ * decoding.  Float buffers must be 16-byte aligned; inputNum values. */
+
+/* Pack inputNum float values into vd_input_size(options, inputNum) bytes of encPack_t words on the
+ * device (a trailing partial word packs missing values as 0.0f). */
+int vd_pack_device(int options, const float* llr_d, size_t inputNum, float scale, void* packed_d, void* stream);
+/* Fused quantise + decode from device floats: the branch-metric table build quantises each value
+ * (no packed intermediate, one kernel).  SOFT16 packs into the decoder's buffer first. */
+int vd_run_device_llr(vd_decoder* dec, const float* llr_d, void* output_d, size_t inputNum, float scale,
+                      void* stream);
+/* Blocking host-to-host variant (H2D of the floats, fused decode, D2H); kernel_ms as in vd_run. */
+int vd_run_llr(vd_decoder* dec, const float* llr_h, void* output_h, size_t inputNum, float scale, float* kernel_ms);
+
 /* ---- synthetic channel source on the GPU (the reference's RandBitGen | ConvolutionalEncoder |
  *      AddNoise | SoftDecisionPacker chain, viterbiDF.h:20-167, is host-side; this is the
  *      product's own device-resident generator for benchmarks: bits from a counter-based hash,

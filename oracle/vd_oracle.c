@@ -515,6 +515,41 @@ int vo_simulate(int opt, size_t N, float snr, uint32_t bitSeed, uint32_t noiseSe
     return 0;
 }
 
+/*
+ * SoftDecisionPacker::process (viterbiDF.h:98-167) on caller-given channel values: quantise v*scale
+ * (quant(), viterbiDF.h:106-125 -- lrintf, then for SOFT4/SOFT8 the long is narrowed to int before
+ * saturating, for SOFT16 saturated as a long) and pack dataPerPack codes MSB-first per 32-bit word;
+ * FP32 writes v*scale (the reference returns src unchanged when scale == 1, identical values).
+ * n values in, vo_input_size(opt, n) bytes out.  A trailing partial word (n not a multiple of
+ * dataPerPack) packs the missing values as 0.0f; the reference reads past the end of its vector there.
+ */
+void vo_pack(int opt, const float* v, size_t n, float scale, void* packed)
+{
+    int ch = CH(opt);
+    if (ch == CH_FP32) {
+        float* pf = (float*)packed;
+        for (size_t i = 0; i < n; i++) pf[i] = scale == 1.0f ? v[i] : v[i] * scale;
+        return;
+    }
+    int packLen = 0, dpp = 0;
+    switch (ch) {
+    case CH_HARD: packLen = 1; dpp = 32; break;
+    case CH_SOFT4: packLen = 4; dpp = 8; break;
+    case CH_SOFT8: packLen = 8; dpp = 4; break;
+    case CH_SOFT16: packLen = 16; dpp = 2; break;
+    default: return;
+    }
+    uint32_t* pw = (uint32_t*)packed;
+    for (size_t i = 0; i < n; i += (size_t)dpp) {
+        uint32_t b = 0;
+        for (size_t j = i; j < i + (size_t)dpp; j++) {
+            float x = j < n ? v[j] : 0.0f;
+            b = (b << packLen) | quant(ch, x * scale);
+        }
+        pw[i / (size_t)dpp] = b;
+    }
+}
+
 /* BER count (main.cpp:151-171): decoded bit i vs source bit i + extraL */
 long long vo_ben(int opt, const uint8_t* bits, size_t N, const void* dec, size_t decBytes)
 {

@@ -44,6 +44,7 @@ def lib():
         L.vo_simulate.argtypes = [ctypes.c_int, sz, ctypes.c_float, ctypes.c_uint32, ctypes.c_uint32,
                                   ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
         L.vo_ben.argtypes = [ctypes.c_int, ctypes.c_void_p, sz, ctypes.c_void_p, sz]
+        L.vo_pack.argtypes = [ctypes.c_int, ctypes.c_void_p, sz, ctypes.c_float, ctypes.c_void_p]
         L.vo_ben.restype = ctypes.c_longlong
         L.vo_gen_bits.argtypes = [ctypes.c_uint32, sz, ctypes.c_void_p]
         L.vo_gen_normals.argtypes = [ctypes.c_uint32, ctypes.c_float, sz, ctypes.c_void_p]
@@ -99,6 +100,15 @@ def decode(opt, packed, input_num=None, nchunks=6400, b16_policy=0, nthreads=Non
     rc = lib().vo_decode(opt, packed.ctypes.data, out.ctypes.data, input_num, nchunks, b16_policy, nthreads)
     assert rc >= 0, rc
     return out, rc == 0
+
+
+def pack(opt, values, scale=40000.0):
+    """SoftDecisionPacker(channel, scale) on float32 channel values (viterbiDF.h:98-167)."""
+    v = np.ascontiguousarray(values, dtype=np.float32)
+    nbytes = input_size(opt, v.size)
+    out = np.zeros((nbytes + 3) // 4, dtype=in_dtype(opt))
+    lib().vo_pack(opt, v.ctypes.data, v.size, scale, out.ctypes.data)
+    return out
 
 
 def ben(opt, bits, dec):

@@ -8,6 +8,14 @@ import sys
 
 import pytest
 
+# torch (device buffers for the device-pointer entry points) ships its own libamdhip64; importing it
+# before libvitdec is loaded makes the library bind to that same HIP runtime (as in bench.py) instead
+# of loading /opt/rocm's second copy, in which case torch reports no GPUs
+try:
+    import torch  # noqa: F401
+except ImportError:
+    pass
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = os.path.join(ROOT, "gpu-accelerated-viterbi-decoder_amd")
 ORACLE = os.path.join(ROOT, "oracle")

@@ -122,3 +122,18 @@ def test_sizes(vo):
     assert vo.input_size(vo.SOFT8, 64_000_000) == 64_000_000
     assert vo.input_size(vo.FP32, 64_000_000) == 256_000_000
     assert vo.message_len(0, 2_000_000) == 999_936
+
+
+@pytest.mark.parametrize("ch", [0, 1, 2, 3, 4])
+def test_packer_matches_harness_pipeline(vo, ch):
+    """vo_pack (SoftDecisionPacker on given floats) equals the harness' own packing of the noiseless
+    BPSK codeword (RandBitGen | ConvolutionalEncoder | AddNoise(+inf) | SoftDecisionPacker)."""
+    n = 4096
+    bits, packed = vo.simulate(ch, n, 0.0, 21, 22, noiseless=True)
+    reg = 0
+    vals = np.empty(2 * n, dtype=np.float32)
+    for i, b in enumerate(bits):
+        reg = ((reg >> 1) | (int(b) << 6)) & 127
+        vals[2 * i] = 1.0 if bin(reg & 0o171).count("1") & 1 else -1.0
+        vals[2 * i + 1] = 1.0 if bin(reg & 0o133).count("1") & 1 else -1.0
+    assert np.array_equal(vo.pack(ch, vals, 40000.0).view(np.uint32), packed.view(np.uint32))
