@@ -121,12 +121,51 @@ def gather_checksums(sums, dev, world):
     return [[int(v) for v in g.cpu()] for g in gathered]
 
 
+def llr_side_measurement(dev, sptr, stream, reps=5):
+    """Float channel values in HBM (the reference's AddNoise output, before SoftDecisionPacker): the GPU
+    packer alone, packer + decode, and the fused decode (quantisation in the table build), SOFT8/int16.
+    Outside the timed region; not part of `value`."""
+    opt = vitdec.SOFT8 | vitdec.M_B16 | vitdec.O_B32
+    n = 2 * N_BITS
+    g = torch.Generator(device=dev)
+    g.manual_seed(5)
+    vals = (torch.randint(0, 2, (n,), device=dev, generator=g).float() * 2 - 1
+            + 0.5 * torch.randn(n, device=dev, generator=g))
+    packed = torch.empty(vitdec.lib().vd_input_size(opt, n), dtype=torch.uint8, device=dev)
+    out_fused = torch.empty(vitdec.lib().vd_output_size(opt, n), dtype=torch.uint8, device=dev)
+    out_two = torch.empty_like(out_fused)
+    dec = vitdec.ViterbiCUDA(opt, 0, dev)
+
+    def timed(fn):
+        fn()
+        e = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+        e[0].record(stream)
+        for _ in range(reps):
+            fn()
+        e[1].record(stream)
+        torch.cuda.synchronize()
+        return e[0].elapsed_time(e[1]) / reps
+
+    pack = lambda: vitdec.pack_device(opt, vals.data_ptr(), n, packed.data_ptr(), 40000.0, sptr)
+    two = lambda: (pack(), dec.run_device(packed.data_ptr(), out_two.data_ptr(), n, sptr))
+    fused = lambda: dec.run_device_llr(vals.data_ptr(), out_fused.data_ptr(), n, 40000.0, sptr)
+    t_pack, t_two, t_fused = timed(pack), timed(two), timed(fused)
+    same = bool(torch.equal(out_fused, out_two))
+    msg = vitdec.lib().vd_message_len(opt, n)
+    dec.close()
+    return {"workload": "64M float32 channel values (32M-bit SOFT8 batch, scale 40000) resident in HBM",
+            "pack_ms": round(t_pack, 4), "pack_GBps": round(n * 4 / (t_pack * 1e-3) / 1e9, 1),
+            "pack_then_decode_ms": round(t_two, 4), "fused_decode_ms": round(t_fused, 4),
+            "fused_gbps": round(msg / (t_fused * 1e-3) / 1e9, 2), "fused_equals_pack_then_decode": same}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-llr", action="store_true", help="skip the float-input (packer fused) side measurement")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -193,6 +232,7 @@ def main():
         out_h = b["out"].cpu().numpy().view(dt)
         bers.append(vitdec.count_errors(b["opt"], bits_h, out_h) / b["msg"])
         sums.append(int(np.bitwise_xor.reduce(out_h.view(np.uint32))))
+    llr = None if args.no_llr else llr_side_measurement(dev, sptr, stream)
     if world > 1:
         elapsed = max_over_ranks(elapsed, dev)
         gathered = gather_checksums(sums, dev, world)
@@ -259,6 +299,8 @@ def main():
             },
             "checksums": [[hex(x) for x in g] for g in gathered],
         }
+        if llr is not None:
+            result["config"]["llr_input"] = llr
         if not args.no_cpu_baseline and world == 1:
             result["cpu_baseline"] = cpu_baseline(batches)
         print(json.dumps(result), flush=True)

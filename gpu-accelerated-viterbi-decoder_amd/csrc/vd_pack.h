@@ -13,10 +13,13 @@
 
 namespace vd {
 
-__device__ __forceinline__ long long lrintf_x86(float v)
+// (int)lrintf(v) for |v| >= 2^31: the low 32 bits of the 64-bit rounded value (v is integral there;
+// v - 2^32 floor(v / 2^32) is exact, a multiple of 256 below 2^32), 0 for NaN and |v| >= 2^63
+__device__ __forceinline__ int narrow_lrintf_x86_big(float v)
 {
-    // |v| < 2^63 (false for NaN): exact conversion of the rounded value; else LONG_MIN
-    return __builtin_fabsf(v) < 9.2233720368547758e18f ? (long long)__builtin_rintf(v) : (long long)(1ull << 63);
+    if (!(__builtin_fabsf(v) < 9.2233720368547758e18f)) return 0;
+    const float r = __builtin_fmaf(-4294967296.0f, __builtin_floorf(v * 2.3283064365386963e-10f), v);  // [0, 2^32)
+    return (int)(uint32_t)r;
 }
 // channel code of one scaled value (CH = HARD 0, SOFT4 1, SOFT8 2, SOFT16 3)
 template <int CH>
@@ -25,12 +28,18 @@ __device__ __forceinline__ uint32_t pack_code(float v)
     if constexpr (CH == 0) {
         return v > 0.0f ? 1u : 0u;
     } else if constexpr (CH == 3) {
-        long long q = lrintf_x86(v);
-        q = q < -32768 ? -32768 : (q > 32767 ? 32767 : q);
+        // lrintf saturated as a long: |v| < 2^63 rounds and clamps (v_cvt_i32 saturates), NaN and
+        // |v| >= 2^63 are LONG_MIN -> -32768
+        int q = __builtin_amdgcn_fmed3f(__builtin_rintf(v), -32768.0f, 32767.0f);
+        if (!(__builtin_fabsf(v) < 9.2233720368547758e18f)) q = -32768;
         return (uint32_t)q & 0xFFFFu;
     } else {
-        int q = (int)(uint32_t)(unsigned long long)lrintf_x86(v);  // narrowing: low 32 bits
         constexpr int lo = CH == 1 ? -8 : -128, hi = CH == 1 ? 7 : 127;
+        int q;
+        if (__builtin_expect(__builtin_fabsf(v) < 2147483648.0f, 1))
+            q = (int)__builtin_rintf(v);  // exact: integral and in int range
+        else
+            q = narrow_lrintf_x86_big(v);
         q = q < lo ? lo : (q > hi ? hi : q);
         return (uint32_t)q & (CH == 1 ? 0xFu : 0xFFu);
     }
