@@ -159,6 +159,25 @@ def llr_side_measurement(dev, sptr, stream, reps=5):
             "fused_gbps": round(msg / (t_fused * 1e-3) / 1e9, 2), "fused_equals_pack_then_decode": same}
 
 
+def pcie_side_measurement(batches, dev, nb=6):
+    """PCIe-inclusive rate (the reference run()'s scope: host buffers in, host buffers out): nb
+    independent batches per workload from pinned host memory through vd_run_stream (H2D of batch b+1,
+    decode of b, D2H of b-1 overlapped).  Outside the timed region; never `value`."""
+    res = {"batches": nb, "host_buffers": "pinned (vd_host_alloc)"}
+    for b in batches:
+        packed = b["inp"].cpu().numpy().view(np.float32 if (b["opt"] & 0xF) == vitdec.FP32 else np.int32)
+        pins = [vitdec.PinnedArray(packed.shape, packed.dtype) for _ in range(nb)]
+        for p in pins:
+            p.array[:] = packed
+        dec = vitdec.ViterbiCUDA(b["opt"], b["input_num"], dev)
+        dec.run_stream([pins[0].array], b["input_num"])  # warm-up (buffers, streams)
+        outs, ms = dec.run_stream([p.array for p in pins], b["input_num"])
+        dec.close()
+        res[b["name"]] = {"wall_ms": round(ms, 3), "gbps": round(nb * b["msg"] / (ms * 1e-3) / 1e9, 2),
+                          "h2d_bytes_per_batch": packed.nbytes}
+    return res
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -166,6 +185,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-llr", action="store_true", help="skip the float-input (packer fused) side measurement")
+    ap.add_argument("--no-pcie", action="store_true", help="skip the host-to-host pipelined side measurement")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -233,6 +253,7 @@ def main():
         bers.append(vitdec.count_errors(b["opt"], bits_h, out_h) / b["msg"])
         sums.append(int(np.bitwise_xor.reduce(out_h.view(np.uint32))))
     llr = None if args.no_llr else llr_side_measurement(dev, sptr, stream)
+    pcie = None if args.no_pcie else pcie_side_measurement(batches, dev)
     if world > 1:
         elapsed = max_over_ranks(elapsed, dev)
         gathered = gather_checksums(sums, dev, world)
@@ -301,6 +322,8 @@ def main():
         }
         if llr is not None:
             result["config"]["llr_input"] = llr
+        if pcie is not None:
+            result["config"]["pcie_inclusive"] = pcie
         if not args.no_cpu_baseline and world == 1:
             result["cpu_baseline"] = cpu_baseline(batches)
         print(json.dumps(result), flush=True)

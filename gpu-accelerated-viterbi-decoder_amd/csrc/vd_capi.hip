@@ -173,6 +173,11 @@ struct vd_decoder {
     size_t cap_in = 0, cap_out = 0, cap_llr = 0;
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    // vd_run_stream: a second buffer set and the copy-in / copy-out streams of the 3-stage pipeline
+    void* in2_d = nullptr;
+    void* out2_d = nullptr;
+    size_t cap2_in = 0, cap2_out = 0;
+    hipStream_t s_in = nullptr, s_out = nullptr;
 };
 
 static int ensure_capacity(vd_decoder* d, size_t inBytes, size_t outBytes)
@@ -288,6 +293,10 @@ int vd_destroy(vd_decoder* d)
     if (d->in_d) (void)hipFree(d->in_d);
     if (d->out_d) (void)hipFree(d->out_d);
     if (d->llr_d) (void)hipFree(d->llr_d);
+    if (d->in2_d) (void)hipFree(d->in2_d);
+    if (d->out2_d) (void)hipFree(d->out2_d);
+    if (d->s_in) (void)hipStreamDestroy(d->s_in);
+    if (d->s_out) (void)hipStreamDestroy(d->s_out);
     if (d->ev0) (void)hipEventDestroy(d->ev0);
     if (d->ev1) (void)hipEventDestroy(d->ev1);
     if (d->stream) (void)hipStreamDestroy(d->stream);
@@ -386,6 +395,97 @@ int vd_run_llr(vd_decoder* d, const float* llr_h, void* output_h, size_t inputNu
     VD_HIP(hipMemcpyAsync(output_h, d->out_d, outB, hipMemcpyDeviceToHost, d->stream));
     VD_HIP(hipStreamSynchronize(d->stream));
     if (kernel_ms) VD_HIP(hipEventElapsedTime(kernel_ms, d->ev0, d->ev1));
+    return VD_OK;
+}
+
+void* vd_host_alloc(size_t bytes)
+{
+    void* p = nullptr;
+    if (hipHostMalloc(&p, bytes ? bytes : 1, hipHostMallocDefault) != hipSuccess) {
+        fail(VD_ERR_NOMEM, "pinned host allocation failed");
+        return nullptr;
+    }
+    return p;
+}
+
+int vd_host_free(void* p)
+{
+    if (p) VD_HIP(hipHostFree(p));
+    return VD_OK;
+}
+
+// Three-stage pipeline over independent batches on one device: H2D of batch b+1 (stream s_in),
+// decode of batch b (the decoder's stream), D2H of batch b-1 (s_out), two device buffer sets.
+// Host buffers at full PCIe rate when pinned (vd_host_alloc); pageable ones work, staged by HIP.
+int vd_run_stream(vd_decoder* d, const void* const* input_h, void* const* output_h, int nbatches, size_t inputNum,
+                  float* wall_ms)
+{
+    if (!d || !input_h || !output_h || nbatches < 0) return fail(VD_ERR_ARG, "bad arguments");
+    if (message_len(d->options, inputNum) == 0) return fail(VD_ERR_ARG, "inputNum too small");
+    const size_t inB = input_size(d->options, inputNum), outB = message_len(d->options, inputNum) / 8;
+    VD_HIP(hipSetDevice(d->device));
+    int rc = ensure_capacity(d, inB, outB + 16);
+    if (rc != VD_OK) return rc;
+    if (inB > d->cap2_in) {
+        if (d->in2_d) (void)hipFree(d->in2_d);
+        d->in2_d = nullptr;
+        d->cap2_in = 0;
+        VD_HIP(hipMalloc(&d->in2_d, inB));
+        d->cap2_in = inB;
+    }
+    if (outB + 16 > d->cap2_out) {
+        if (d->out2_d) (void)hipFree(d->out2_d);
+        d->out2_d = nullptr;
+        d->cap2_out = 0;
+        VD_HIP(hipMalloc(&d->out2_d, outB + 16));
+        d->cap2_out = outB + 16;
+    }
+    if (!d->s_in) VD_HIP(hipStreamCreateWithFlags(&d->s_in, hipStreamNonBlocking));
+    if (!d->s_out) VD_HIP(hipStreamCreateWithFlags(&d->s_out, hipStreamNonBlocking));
+    void* ins[2] = {d->in_d, d->in2_d};
+    void* outs[2] = {d->out_d, d->out2_d};
+    // per buffer set: input landed, decode done (input free, output ready), output drained
+    hipEvent_t landed[2], decoded[2], drained[2];
+    for (int k = 0; k < 2; k++) {
+        VD_HIP(hipEventCreateWithFlags(&landed[k], hipEventDisableTiming));
+        VD_HIP(hipEventCreateWithFlags(&decoded[k], hipEventDisableTiming));
+        VD_HIP(hipEventCreateWithFlags(&drained[k], hipEventDisableTiming));
+    }
+    auto t0 = std::chrono::steady_clock::now();
+    rc = VD_OK;
+    for (int b = 0; b < nbatches && rc == VD_OK; b++) {
+        const int k = b & 1;
+        if (b >= 2) {  // set k is reused: its previous decode must have consumed the input
+            if (hipStreamWaitEvent(d->s_in, decoded[k], 0) != hipSuccess) { rc = fail(VD_ERR_DEVICE, "wait"); break; }
+        }
+        if (hipMemcpyAsync(ins[k], input_h[b], inB, hipMemcpyHostToDevice, d->s_in) != hipSuccess ||
+            hipEventRecord(landed[k], d->s_in) != hipSuccess ||
+            hipStreamWaitEvent(d->stream, landed[k], 0) != hipSuccess ||
+            (b >= 2 && hipStreamWaitEvent(d->stream, drained[k], 0) != hipSuccess)) {
+            rc = fail(VD_ERR_DEVICE, "pipeline enqueue failed");
+            break;
+        }
+        rc = launch_decode(d->options, ins[k], outs[k], inputNum, d->stream);
+        if (rc != VD_OK) break;
+        if (hipEventRecord(decoded[k], d->stream) != hipSuccess ||
+            hipStreamWaitEvent(d->s_out, decoded[k], 0) != hipSuccess ||
+            hipMemcpyAsync(output_h[b], outs[k], outB, hipMemcpyDeviceToHost, d->s_out) != hipSuccess ||
+            hipEventRecord(drained[k], d->s_out) != hipSuccess) {
+            rc = fail(VD_ERR_DEVICE, "pipeline enqueue failed");
+            break;
+        }
+    }
+    const hipError_t e1 = hipStreamSynchronize(d->s_out), e2 = hipStreamSynchronize(d->stream),
+                     e3 = hipStreamSynchronize(d->s_in);
+    auto t1 = std::chrono::steady_clock::now();
+    for (int k = 0; k < 2; k++) {
+        (void)hipEventDestroy(landed[k]);
+        (void)hipEventDestroy(decoded[k]);
+        (void)hipEventDestroy(drained[k]);
+    }
+    if (rc != VD_OK) return rc;
+    if (e1 != hipSuccess || e2 != hipSuccess || e3 != hipSuccess) return fail(VD_ERR_DEVICE, "pipeline failed");
+    if (wall_ms) *wall_ms = std::chrono::duration<float, std::milli>(t1 - t0).count();
     return VD_OK;
 }
 

@@ -41,7 +41,8 @@ _ERRNAMES = {-1: "VD_ERR_OPTIONS", -2: "VD_ERR_ARG", -3: "VD_ERR_DEVICE", -4: "V
 EXPORTS = ["vd_options_valid", "vd_input_size", "vd_message_len", "vd_output_size", "vd_num_chunks",
            "vd_create", "vd_destroy", "vd_run", "vd_run_device", "vd_run_batches", "vd_synth_device",
            "vd_simulate_host", "vd_count_errors", "vd_last_error", "vd_device_count", "vd_kernel_name",
-           "vd_pack_device", "vd_run_device_llr", "vd_run_llr"]
+           "vd_pack_device", "vd_run_device_llr", "vd_run_llr", "vd_host_alloc", "vd_host_free",
+           "vd_run_stream"]
 
 
 class VitdecError(RuntimeError):
@@ -76,6 +77,10 @@ def lib():
     L.vd_count_errors.restype = ctypes.c_longlong
     L.vd_last_error.restype = ctypes.c_char_p
     L.vd_pack_device.argtypes = [i, vp, sz, f, vp, vp]
+    L.vd_host_alloc.argtypes = [sz]
+    L.vd_host_alloc.restype = vp
+    L.vd_host_free.argtypes = [vp]
+    L.vd_run_stream.argtypes = [vp, ctypes.POINTER(vp), ctypes.POINTER(vp), i, sz, ctypes.POINTER(f)]
     L.vd_run_device_llr.argtypes = [vp, vp, vp, sz, f, vp]
     L.vd_run_llr.argtypes = [vp, vp, vp, sz, f, ctypes.POINTER(f)]
     L.vd_kernel_name.argtypes = [i]
@@ -191,6 +196,24 @@ class ViterbiCUDA:
                                    ctypes.c_void_p(stream)))
 
 
+    def run_stream(self, inputs, inputNum=None, outputs=None):
+        """Pipelined decode of independent batches (host copies overlapped with decoding).
+        Returns (list of outputs, wall ms).  Pass pinned arrays (pinned_empty) for full PCIe rate."""
+        inputs = [np.ascontiguousarray(a) for a in inputs]
+        if inputNum is None:
+            inputNum = inputs[0].size * self.encDataPerPack
+        n_out = self.getOutputSize(inputNum) // np.dtype(self.decPack_t).itemsize
+        if outputs is None:
+            outputs = [np.zeros(n_out, dtype=self.decPack_t) for _ in inputs]
+        for a in inputs:
+            if a.nbytes < self.getInputSize(inputNum):
+                raise VitdecError("input buffer smaller than getInputSize(inputNum)")
+        ins = (ctypes.c_void_p * len(inputs))(*[a.ctypes.data for a in inputs])
+        outs = (ctypes.c_void_p * len(outputs))(*[o.ctypes.data for o in outputs])
+        ms = ctypes.c_float(0.0)
+        _check(lib().vd_run_stream(self._h, ins, outs, len(inputs), inputNum, ctypes.byref(ms)))
+        return outputs, ms.value
+
     # ---- float channel values (SoftDecisionPacker(channel, scale) fused into the decode) ----
     def run_llr(self, llr_h, scale=40000.0, output_h=None):
         """Blocking decode of float channel values (viterbiDF.h:98-167 packer fused). Returns (out, ms)."""
@@ -207,6 +230,23 @@ class ViterbiCUDA:
         """Async fused decode of inputNum device floats (16-byte aligned)."""
         _check(lib().vd_run_device_llr(self._h, ctypes.c_void_p(llr_ptr), ctypes.c_void_p(output_ptr), inputNum,
                                        scale, ctypes.c_void_p(stream)))
+
+
+class PinnedArray:
+    """A numpy view of page-locked host memory from vd_host_alloc (freed with the object)."""
+
+    def __init__(self, shape, dtype):
+        n = int(np.prod(shape)) * np.dtype(dtype).itemsize
+        self._p = lib().vd_host_alloc(n)
+        if not self._p:
+            raise VitdecError("vd_host_alloc failed")
+        buf = (ctypes.c_char * n).from_address(self._p)
+        self.array = np.frombuffer(buf, dtype=dtype).reshape(shape)
+
+    def __del__(self):
+        if getattr(self, "_p", None):
+            lib().vd_host_free(self._p)
+            self._p = None
 
 
 def pack_device(options, llr_ptr, inputNum, packed_ptr, scale=40000.0, stream=0):

@@ -80,6 +80,19 @@ int vd_run_device(vd_decoder* dec, const void* input_d, void* output_d, size_t i
 int vd_run_batches(int options, const void* const* input_h, void* const* output_h, size_t inputNum,
                    int nbatches, const int* devices, int ndev, float* wall_ms);
 
+/* ---- streaming host pipeline (the reference allocates, copies and frees per call,
+ *      viterbi.cu:210-238) ---- */
+
+/* Pinned (page-locked) host buffers for full-rate PCIe copies; NULL on failure. */
+void* vd_host_alloc(size_t bytes);
+int vd_host_free(void* p);
+/* Decode nbatches independent batches (input_h[b] -> output_h[b], inputNum encoded values each) on
+ * the decoder's device with the host copies overlapped: H2D of batch b+1, decode of batch b and D2H
+ * of batch b-1 run concurrently (two device buffer sets, three streams).  Each result equals vd_run
+ * of that batch.  wall_ms (optional): wall time of the whole call. */
+int vd_run_stream(vd_decoder* dec, const void* const* input_h, void* const* output_h, int nbatches, size_t inputNum,
+                  float* wall_ms);
+
 /* ---- float channel values (the reference's SoftDecisionPacker stage, viterbiDF.h:98-167) ----
  * The reference packs float channel values on the host (quant(v*scale): HARD v > 0; SOFT4/SOFT8
  * (int)lrintf saturated to 4/8 bits; SOFT16 lrintf saturated to 16 bits; FP32 v*scale; MSB-first

@@ -68,3 +68,30 @@ def test_run_device_stream_ordered(gpu, vo):
         d.run_device(inp.data_ptr(), out.data_ptr(), 2_000_000, s.cuda_stream)
     s.synchronize()
     np.testing.assert_array_equal(out.cpu().numpy().view(np.uint32), ref)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("pinned", [False, True])
+def test_run_stream_matches_run(gpu, vo, pinned):
+    # the overlapped H2D / decode / D2H pipeline over independent batches: every batch as vd_run
+    opt = gpu.SOFT8 | gpu.M_B16
+    n_bits = 400_000
+    batches = [vo.simulate(opt, n_bits, 1.0, 30 + b, 60 + b)[1] for b in range(5)]
+    refs = [vo.decode(opt, p)[0] for p in batches]
+    keep = []
+    if pinned:
+        ins = []
+        for p in batches:
+            a = gpu.PinnedArray(p.shape, p.dtype)
+            a.array[:] = p
+            keep.append(a)
+            ins.append(a.array)
+    else:
+        ins = batches
+    with gpu.ViterbiCUDA(opt) as d:
+        outs, ms = d.run_stream(ins)
+        single = [d.run(p)[0] for p in batches]
+    assert ms > 0
+    for o, s, r in zip(outs, single, refs):
+        np.testing.assert_array_equal(o, r)
+        np.testing.assert_array_equal(s, r)
