@@ -87,9 +87,12 @@ int vd_run_batches(int options, const void* const* input_h, void* const* output_
 void* vd_host_alloc(size_t bytes);
 int vd_host_free(void* p);
 /* Decode nbatches independent batches (input_h[b] -> output_h[b], inputNum encoded values each) on
- * the decoder's device with the host copies overlapped: H2D of batch b+1, decode of batch b and D2H
- * of batch b-1 run concurrently (two device buffer sets, three streams).  Each result equals vd_run
- * of that batch.  wall_ms (optional): wall time of the whole call. */
+ * the decoder's device.  Pinned buffers (vd_host_alloc, hipHostMalloc, hipHostRegister): the decode
+ * kernels read the packed input from and write the decoded words to host memory directly over PCIe
+ * (zero-copy, no staging).  Pageable buffers: H2D of batch b+1, decode of batch b and D2H of batch
+ * b-1 overlap (two device buffer sets, three streams).  Each result equals vd_run of that batch.
+ * wall_ms (optional): wall time of the whole call.  (vd_run also decodes zero-copy when both of its
+ * host buffers are pinned.) */
 int vd_run_stream(vd_decoder* dec, const void* const* input_h, void* const* output_h, int nbatches, size_t inputNum,
                   float* wall_ms);
 

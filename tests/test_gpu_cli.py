@@ -88,9 +88,19 @@ def test_run_stream_matches_run(gpu, vo, pinned):
             ins.append(a.array)
     else:
         ins = batches
+    outs_in = None
+    if pinned:  # pinned inputs AND outputs: the zero-copy path (kernels read/write host memory)
+        n_out = refs[0].size
+        pouts = [gpu.PinnedArray((n_out,), np.uint32) for _ in batches]
+        keep += pouts
+        outs_in = [o.array for o in pouts]
     with gpu.ViterbiCUDA(opt) as d:
-        outs, ms = d.run_stream(ins)
+        outs, ms = d.run_stream(ins, outputs=outs_in)
         single = [d.run(p)[0] for p in batches]
+        if pinned:  # vd_run with both buffers pinned decodes zero-copy as well
+            z = gpu.PinnedArray(refs[0].shape, np.uint32)
+            d.run(ins[0], z.array)
+            np.testing.assert_array_equal(z.array, refs[0])
     assert ms > 0
     for o, s, r in zip(outs, single, refs):
         np.testing.assert_array_equal(o, r)
