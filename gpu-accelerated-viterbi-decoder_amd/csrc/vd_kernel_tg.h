@@ -76,15 +76,7 @@ __device__ __forceinline__ int tg_pos(int l)
     const int p2 = (l >> 2) & 1;
     return (l & ~7) | (p2 << 2) | ((((l >> 1) & 1) ^ p2) << 1) | ((l & 1) ^ p2);
 }
-// 1 where the reference lets the own predecessor win ties (viterbiACS.cuh:113-157,216-256)
-template <int CORE>
-__device__ __forceinline__ int tg_cls(int p, int K)
-{
-    if constexpr (CORE == F16) return 1;
-    else if constexpr (CORE == B16) return 0;
-    else return (K == 0 && (p & 32)) ? 1 : 0;
-}
-// label flip of the butterfly partner in a swap stage: own_label(p ^ (1 << q), K) = own_label(p, K) ^ d
+// reference label (0..3) of position p's own predecessor branch at stage phase k, and its parity helper
 __host__ __device__ constexpr int tg_par7(int v) { return (v & 1) ^ ((v >> 1) & 1) ^ ((v >> 2) & 1) ^ ((v >> 3) & 1) ^ ((v >> 4) & 1) ^ ((v >> 5) & 1) ^ ((v >> 6) & 1); }
 __host__ __device__ constexpr int tg_label(int p, int k)
 {

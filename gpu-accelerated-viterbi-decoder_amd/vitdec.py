@@ -198,7 +198,7 @@ class ViterbiCUDA:
 
     def run_stream(self, inputs, inputNum=None, outputs=None):
         """Pipelined decode of independent batches (host copies overlapped with decoding).
-        Returns (list of outputs, wall ms).  Pass pinned arrays (pinned_empty) for full PCIe rate."""
+        Returns (list of outputs, wall ms).  Pass PinnedArray(...).array buffers (inputs and outputs) for the zero-copy path."""
         inputs = [np.ascontiguousarray(a) for a in inputs]
         if inputNum is None:
             inputNum = inputs[0].size * self.encDataPerPack
