@@ -6,6 +6,7 @@
 // sync-free device path; vd_run_batches shards independent batches over the devices of a node.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -20,6 +21,8 @@
 #include "vd_kernel_tg.h"
 #include "vd_pack.h"
 #include "vd_synth.h"
+#include "vd_mt.h"
+#include "vd_mtjump.h"
 
 namespace {
 
@@ -595,3 +598,126 @@ int vd_synth_device(int options, size_t N, float snr, uint64_t seed, void* bits_
 }
 
 }  // extern "C"
+
+// ---------------------------------------------------------------- reference-exact channel source
+namespace {
+constexpr uint64_t kMtL = 65536;  // engine outputs per parallel segment
+constexpr int kMtR = 4;           // radix of the jump tree
+constexpr int kMtLevels = 8;      // jump polynomials for trees of up to R^8 = 65536 segments (2^32 outputs)
+int mt_levels(uint64_t T)
+{
+    int k = 0;
+    for (uint64_t p = 1; p < T; p *= kMtR) k++;
+    return k;
+}
+// segment-start states of std::mt19937(seed) for T segments of kMtL outputs: st[m] = the state after
+// m * kMtL outputs.  Jump tree, top level first: every state at a multiple of R^(k+1) generates its
+// raw words (mt_xseq), then the R-1 children at +c R^k are XOR-accumulated from them (mt_jump).
+int mt_states(uint32_t seed, uint64_t T, uint32_t* st, uint32_t* xs, uint32_t* polys_d, hipStream_t s)
+{
+    using namespace vd::mt;
+    VD_HIP(hipMemsetAsync(st, 0, T * kN * 4, s));
+    hipLaunchKernelGGL(mt_seed, dim3(1), dim3(64), 0, s, seed, st);
+    VD_HIP(hipGetLastError());
+    const int levels = mt_levels(T);
+    if (!levels) return VD_OK;
+    if (levels > kMtLevels) return fail(VD_ERR_ARG, "mt19937 stream longer than the jump tree");
+    const std::vector<uint32_t>* polys;
+    try {
+        polys = &vd::mtj::jump_polys(kMtL, kMtR, kMtLevels);  // level k's polynomials do not depend on the depth
+    } catch (const std::exception& e) {
+        return fail(VD_ERR_DEVICE, std::string("mt19937 jump polynomials: ") + e.what());
+    }
+    VD_HIP(hipMemcpyAsync(polys_d, polys->data(), polys->size() * 4, hipMemcpyHostToDevice, s));
+    uint64_t step = 1;
+    for (int k = 0; k < levels; k++) step *= kMtR;  // R^levels
+    for (int k = levels - 1; k >= 0; k--) {
+        const uint64_t dstStep = step / kMtR, nsrc = (T + step - 1) / step;
+        hipLaunchKernelGGL(mt_xseq, dim3((unsigned)nsrc), dim3(kThreads), 0, s, st, (uint32_t)step, xs);
+        VD_HIP(hipGetLastError());
+        hipLaunchKernelGGL(mt_jump, dim3((unsigned)nsrc, kMtR - 1, (kQW + kSliceWords - 1) / kSliceWords), dim3(640), 0,
+                           s, xs, polys_d + (size_t)k * (kMtR - 1) * kQW, (uint32_t)step, (uint32_t)dstStep, (uint32_t)T, st);
+        VD_HIP(hipGetLastError());
+        step = dstStep;
+    }
+    return VD_OK;
+}
+struct DevBuf {  // stream-ordered scratch
+    void* p = nullptr;
+    hipStream_t s;
+    explicit DevBuf(hipStream_t s_) : s(s_) {}
+    hipError_t alloc(size_t n) { return hipMallocAsync(&p, n ? n : 4, s); }
+    ~DevBuf() { if (p) (void)hipFreeAsync(p, s); }
+};
+}  // namespace
+
+extern "C" {
+
+int vd_channel_device(size_t N, float snr, uint32_t bitSeed, uint32_t noiseSeed, uint8_t* bits_d, float* values_d,
+                      void* stream)
+{
+    using namespace vd::mt;
+    if (!bits_d || !values_d) return fail(VD_ERR_ARG, "null argument");
+    if (N == 0) return VD_OK;
+    if (N > (1ull << 30)) return fail(VD_ERR_ARG, "N above 2^30 bits");
+    hipStream_t s = (hipStream_t)stream;
+    const float sigma = (float)std::pow(10, -snr / 5.0);  // AddNoise(pow(10, -snr/5.0)), main.cpp:135
+    const uint64_t nval = 2 * (uint64_t)N;
+    // message bits
+    const uint64_t Tb = (N + kMtL - 1) / kMtL;
+    const uint64_t attempts = std::isinf(sigma) ? 0 : (uint64_t)(1.30 * (double)N) + 4096;  // E = 4/pi N
+    const uint64_t Tn = (2 * attempts + kMtL - 1) / kMtL;
+    const uint64_t Tmax = std::max(Tb, Tn);
+    const uint64_t nxs = (Tmax + kMtR - 1) / kMtR;
+    DevBuf stb(s), stn(s), xs(s), pol(s), cnt(s);
+    VD_HIP(stb.alloc(Tb * kN * 4));
+    VD_HIP(xs.alloc(nxs * kNX * 4));
+    VD_HIP(pol.alloc((size_t)kMtLevels * (kMtR - 1) * kQW * 4));
+    int rc = mt_states(bitSeed, Tb, (uint32_t*)stb.p, (uint32_t*)xs.p, (uint32_t*)pol.p, s);
+    if (rc) return rc;
+    hipLaunchKernelGGL(mt_bits, dim3((unsigned)Tb), dim3(kThreads), 0, s, (const uint32_t*)stb.p, kMtL, (uint64_t)N, bits_d);
+    VD_HIP(hipGetLastError());
+    if (std::isinf(sigma)) {  // AddNoise's stddev = +inf branch (viterbiDF.h:79-85)
+        hipLaunchKernelGGL(mt_noiseless, dim3((unsigned)((nval + 255) / 256)), dim3(256), 0, s, bits_d, nval, values_d);
+        VD_HIP(hipGetLastError());
+        return VD_OK;
+    }
+    VD_HIP(stn.alloc(Tn * kN * 4));
+    VD_HIP(cnt.alloc((Tn + 1) * 4));
+    rc = mt_states(noiseSeed, Tn, (uint32_t*)stn.p, (uint32_t*)xs.p, (uint32_t*)pol.p, s);
+    if (rc) return rc;
+    uint32_t* counts = (uint32_t*)cnt.p;
+    hipLaunchKernelGGL(mt_noise<0>, dim3((unsigned)Tn), dim3(kThreads), 0, s, (const uint32_t*)stn.p, kMtL, counts,
+                       (const uint8_t*)bits_d, nval, sigma, values_d);
+    VD_HIP(hipGetLastError());
+    hipLaunchKernelGGL(scan_counts, dim3(1), dim3(1024), 0, s, counts, (uint32_t)Tn);
+    VD_HIP(hipGetLastError());
+    hipLaunchKernelGGL(mt_noise<1>, dim3((unsigned)Tn), dim3(kThreads), 0, s, (const uint32_t*)stn.p, kMtL, counts,
+                       (const uint8_t*)bits_d, nval, sigma, values_d);
+    VD_HIP(hipGetLastError());
+    uint32_t total = 0;
+    VD_HIP(hipMemcpyAsync(&total, counts + Tn, 4, hipMemcpyDeviceToHost, s));
+    VD_HIP(hipStreamSynchronize(s));
+    if (total < N) return fail(VD_ERR_DEVICE, "polar method: too few accepted pairs generated");
+    return VD_OK;
+}
+
+int vd_simulate_device(int options, size_t N, float snr, uint32_t bitSeed, uint32_t noiseSeed, uint8_t* bits_d,
+                       void* packed_d, void* stream)
+{
+    if (!valid(options)) return fail(VD_ERR_OPTIONS, "options disabled by OptionsValid");
+    if (!packed_d || N % 16) return fail(VD_ERR_ARG, "null argument or N not a multiple of 16");
+    hipStream_t s = (hipStream_t)stream;
+    DevBuf bb(s), vb(s);
+    if (!bits_d) {
+        VD_HIP(bb.alloc(N));
+        bits_d = (uint8_t*)bb.p;
+    }
+    VD_HIP(vb.alloc(2 * N * sizeof(float)));
+    int rc = vd_channel_device(N, snr, bitSeed, noiseSeed, bits_d, (float*)vb.p, stream);
+    if (rc) return rc;
+    return launch_pack(options, (const float*)vb.p, 2 * N, 40000.0f, packed_d, s);  // SoftDecisionPacker(type, 40000)
+}
+
+}  // extern "C"
+

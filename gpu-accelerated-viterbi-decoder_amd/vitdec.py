@@ -42,7 +42,7 @@ EXPORTS = ["vd_options_valid", "vd_input_size", "vd_message_len", "vd_output_siz
            "vd_create", "vd_destroy", "vd_run", "vd_run_device", "vd_run_batches", "vd_synth_device",
            "vd_simulate_host", "vd_count_errors", "vd_last_error", "vd_device_count", "vd_kernel_name",
            "vd_pack_device", "vd_run_device_llr", "vd_run_llr", "vd_host_alloc", "vd_host_free",
-           "vd_run_stream"]
+           "vd_run_stream", "vd_channel_device", "vd_simulate_device", "vd_mt_state_after"]
 
 
 class VitdecError(RuntimeError):
@@ -73,6 +73,9 @@ def lib():
                                  ctypes.POINTER(f)]
     L.vd_synth_device.argtypes = [i, sz, f, ctypes.c_uint64, vp, vp, vp]
     L.vd_simulate_host.argtypes = [i, sz, f, ctypes.c_uint32, ctypes.c_uint32, vp, vp]
+    L.vd_channel_device.argtypes = [sz, f, ctypes.c_uint32, ctypes.c_uint32, vp, vp, vp]
+    L.vd_simulate_device.argtypes = [i, sz, f, ctypes.c_uint32, ctypes.c_uint32, vp, vp, vp]
+    L.vd_mt_state_after.argtypes = [ctypes.c_uint32, ctypes.c_uint64, vp]
     L.vd_count_errors.argtypes = [i, vp, sz, vp, sz]
     L.vd_count_errors.restype = ctypes.c_longlong
     L.vd_last_error.restype = ctypes.c_char_p
@@ -268,6 +271,27 @@ def simulate_host(options, n_bits, snr, bit_seed, noise_seed):
     packed = np.zeros(nbytes // 4, dtype=np.float32 if (options & CHANNEL_MASK) == FP32 else np.int32)
     _check(lib().vd_simulate_host(options, n_bits, snr, bit_seed, noise_seed, bits.ctypes.data, packed.ctypes.data))
     return bits, packed
+
+
+def channel_device(n_bits, snr, bit_seed, noise_seed, bits_ptr, values_ptr, stream=0):
+    """The reference harness's RandBitGen | ConvolutionalEncoder | AddNoise on the GPU, bit-exact with
+    simulate_host for the same seeds: n_bits bytes of message bits, 2 n_bits float channel values."""
+    _check(lib().vd_channel_device(n_bits, snr, bit_seed, noise_seed, ctypes.c_void_p(bits_ptr),
+                                   ctypes.c_void_p(values_ptr), ctypes.c_void_p(stream)))
+
+
+def simulate_device(options, n_bits, snr, bit_seed, noise_seed, bits_ptr, packed_ptr, stream=0):
+    """channel_device + SoftDecisionPacker(type, 40000): the packed input simulate_host makes, on the GPU."""
+    _check(lib().vd_simulate_device(options, n_bits, snr, bit_seed, noise_seed,
+                                    ctypes.c_void_p(bits_ptr) if bits_ptr else None, ctypes.c_void_p(packed_ptr),
+                                    ctypes.c_void_p(stream)))
+
+
+def mt_state_after(seed, n):
+    """std::mt19937(seed)'s state array after n outputs (host GF(2) jump-ahead used by channel_device)."""
+    st = np.zeros(624, dtype=np.uint32)
+    _check(lib().vd_mt_state_after(seed, n, st.ctypes.data))
+    return st
 
 
 def count_errors(options, bits, decoded):

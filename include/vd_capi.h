@@ -128,6 +128,19 @@ int vd_synth_device(int options, size_t N, float snr, uint64_t seed, void* bits_
  * noise, exactly the reference pipeline's semantics, viterbiDF.h:20-167, main.cpp:131-137). */
 int vd_simulate_host(int options, size_t N, float snr, uint32_t bitSeed, uint32_t noiseSeed,
                      uint8_t* bits, void* packed);
+/* The reference harness's channel source on the GPU, bit-exact with vd_simulate_host for the same
+ * seeds: RandBitGen(N, bitSeed) | ConvolutionalEncoder(7, 0171, 0133) | AddNoise(10^(-snr/5), noiseSeed)
+ * (viterbiDF.h:20-95; std::mt19937 streams generated in parallel segments from a GF(2) jump-ahead,
+ * libstdc++ uniform/normal and glibc logf restated).  bits_d: N bytes (0/1); values_d: 2N floats, the
+ * AddNoise output.  Blocking (checks the polar method's sample count).  N <= 2^30. */
+int vd_channel_device(size_t N, float snr, uint32_t bitSeed, uint32_t noiseSeed, uint8_t* bits_d, float* values_d,
+                      void* stream);
+/* vd_channel_device followed by SoftDecisionPacker(type, 40000) (viterbiDF.h:98-167): packed_d gets
+ * vd_input_size(options, 2N) bytes, identical to vd_simulate_host's.  bits_d may be NULL.  N % 16 == 0. */
+int vd_simulate_device(int options, size_t N, float snr, uint32_t bitSeed, uint32_t noiseSeed, uint8_t* bits_d,
+                       void* packed_d, void* stream);
+/* test hook: std::mt19937(seed)'s 624-word state array after n outputs (host GF(2) jump-ahead) */
+int vd_mt_state_after(uint32_t seed, uint64_t n, uint32_t* state624);
 /* bit-error count of a decoded buffer against the source bits (main.cpp:151-171) */
 long long vd_count_errors(int options, const uint8_t* bits, size_t N, const void* decoded, size_t decodedBytes);
 

@@ -459,6 +459,79 @@ void vo_gen_normals(uint32_t seed, float stddev, size_t n, float* out)
     for (size_t i = 0; i < n; i++) out[i] = normal_draw(&d, &m);
 }
 
+/* raw std::mt19937(seed) outputs n0 .. n0+n-1 (for the jump-ahead tests) */
+void vo_mt_raw(uint32_t seed, size_t n0, size_t n, uint32_t* out)
+{
+    mt19937_t m; mt_seed(&m, seed);
+    for (size_t i = 0; i < n0; i++) (void)mt_next(&m);
+    for (size_t i = 0; i < n; i++) out[i] = mt_next(&m);
+}
+
+/*
+ * glibc 2.35 logf (x86-64 FMA variant, e_logf.c of the ARM optimized-routines, table __logf_data;
+ * the variant glibc's ifunc selects on FMA/AVX2 hosts), restated with its table constants read from
+ * this image's libm.  The GPU channel source (csrc/vd_mt.h glibc_logf) uses the same constants;
+ * vo_logf_mismatch checks the restatement against the host logf.
+ */
+static const double vo_logf_tab[16][2] = {
+    {0x1.661ec79f8f3bep+0, -0x1.57bf7808caadep-2}, {0x1.571ed4aaf883dp+0, -0x1.2bef0a7c06ddbp-2},
+    {0x1.49539f0f010b0p+0, -0x1.01eae7f513a67p-2}, {0x1.3c995b0b80385p+0, -0x1.b31d8a68224e9p-3},
+    {0x1.30d190c8864a5p+0, -0x1.6574f0ac07758p-3}, {0x1.25e227b0b8ea0p+0, -0x1.1aa2bc79c8100p-3},
+    {0x1.1bb4a4a1a343fp+0, -0x1.a4e76ce8c0e5ep-4}, {0x1.12358f08ae5bap+0, -0x1.1973c5a611cccp-4},
+    {0x1.0953f419900a7p+0, -0x1.252f438e10c1ep-5}, {0x1.0000000000000p+0, 0x0.0p+0},
+    {0x1.e608cfd9a47acp-1, 0x1.aa5aa5df25984p-5}, {0x1.ca4b31f026aa0p-1, 0x1.c5e53aa362eb4p-4},
+    {0x1.b2036576afce6p-1, 0x1.526e57720db08p-3}, {0x1.9c2d163a1aa2dp-1, 0x1.bc2860d224770p-3},
+    {0x1.886e6037841edp-1, 0x1.1058bc8a07ee1p-2}, {0x1.767dcf5534862p-1, 0x1.4043057b6ee09p-2}};
+float vo_logf_restated(float x)
+{
+    uint32_t ix; memcpy(&ix, &x, 4);
+    if (ix == 0x3f800000u) return 0.0f;
+    uint32_t tmp = ix - 0x3f330000u, iz = ix - (tmp & 0xff800000u);
+    int i = (int)((tmp >> 19) & 15), k = (int32_t)tmp >> 23;
+    float zf; memcpy(&zf, &iz, 4);
+    double z = zf;
+    double r = fma(z, vo_logf_tab[i][0], -1.0);
+    double y0 = fma((double)k, 0x1.62e42fefa39efp-1, vo_logf_tab[i][1]);
+    double y = fma(r, 0x1.5575b0be00b6ap-2, -0x1.ffffef20a4123p-2);
+    double r2 = r * r;
+    y = fma(r2, -0x1.00ea348b88334p-2, y);
+    y = fma(r2, y, y0 + r);
+    return (float)y;
+}
+/* floats with bit patterns lo, lo+stride, .. <= hi where vo_logf_restated differs from logf */
+long long vo_logf_mismatch(uint32_t lo, uint32_t hi, uint32_t stride)
+{
+    long long bad = 0;
+    for (uint64_t b = lo; b <= hi; b += stride) {
+        uint32_t u = (uint32_t)b;
+        float x; memcpy(&x, &u, 4);
+        float a = logf(x), c = vo_logf_restated(x);
+        if (memcmp(&a, &c, 4)) bad++;
+    }
+    return bad;
+}
+
+/* RandBitGen | ConvolutionalEncoder | AddNoise (viterbiDF.h:20-95): N bits, 2N float values */
+void vo_channel(size_t N, float snr, uint32_t bitSeed, uint32_t noiseSeed, int noiseless, uint8_t* bits,
+                float* values)
+{
+    mt19937_t mb; mt_seed(&mb, bitSeed);
+    for (size_t i = 0; i < N; i++) bits[i] = (uint8_t)(mt_next(&mb) >> 31);
+    float stddev = (float)pow(10.0, (double)(-snr) / 5.0);
+    mt19937_t mn; mt_seed(&mn, noiseSeed);
+    normal_t nd = { 0, 0.0f, stddev };
+    uint32_t buf = 0;
+    for (size_t i = 0; i < N; i++) {
+        buf >>= 1;
+        buf |= (uint32_t)bits[i] << (CL - 1);
+        int o[2] = { parity7((int)(buf & POLY0)), parity7((int)(buf & POLY1)) };
+        for (int j = 0; j < 2; j++) {
+            float base = o[j] ? 1.0f : -1.0f;
+            values[2 * i + j] = noiseless ? base : base + normal_draw(&nd, &mn);
+        }
+    }
+}
+
 static inline uint32_t quant(int ch, float v)
 {
     switch (ch) {

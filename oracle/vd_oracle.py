@@ -48,6 +48,13 @@ def lib():
         L.vo_ben.restype = ctypes.c_longlong
         L.vo_gen_bits.argtypes = [ctypes.c_uint32, sz, ctypes.c_void_p]
         L.vo_gen_normals.argtypes = [ctypes.c_uint32, ctypes.c_float, sz, ctypes.c_void_p]
+        L.vo_mt_raw.argtypes = [ctypes.c_uint32, sz, sz, ctypes.c_void_p]
+        L.vo_logf_restated.argtypes = [ctypes.c_float]
+        L.vo_logf_restated.restype = ctypes.c_float
+        L.vo_logf_mismatch.argtypes = [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32]
+        L.vo_logf_mismatch.restype = ctypes.c_longlong
+        L.vo_channel.argtypes = [sz, ctypes.c_float, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int,
+                                 ctypes.c_void_p, ctypes.c_void_p]
         L.vo_std_bits.argtypes = [ctypes.c_uint32, sz, ctypes.c_void_p]
         L.vo_std_normals.argtypes = [ctypes.c_uint32, ctypes.c_float, sz, ctypes.c_void_p]
         _lib = L
@@ -128,3 +135,23 @@ def gen_normals(seed, stddev, n, use_std=False):
     else:
         lib().vo_gen_normals(seed, stddev, n, out.ctypes.data)
     return out
+
+
+def mt_raw(seed, n0, n):
+    """raw std::mt19937(seed) outputs n0 .. n0+n-1"""
+    out = np.zeros(n, dtype=np.uint32)
+    lib().vo_mt_raw(seed, n0, n, out.ctypes.data)
+    return out
+
+
+def logf_mismatch(lo=0x00800000, hi=0x3F800000, stride=1):
+    """count of floats (bit patterns lo..hi step stride) where the restated glibc logf != host logf"""
+    return int(lib().vo_logf_mismatch(lo, hi, stride))
+
+
+def channel(n_bits, snr, bit_seed, noise_seed, noiseless=False):
+    """RandBitGen | ConvolutionalEncoder | AddNoise: (bits uint8[N], values float32[2N])"""
+    bits = np.zeros(n_bits, dtype=np.uint8)
+    vals = np.zeros(2 * n_bits, dtype=np.float32)
+    lib().vo_channel(n_bits, snr, bit_seed, noise_seed, 1 if noiseless else 0, bits.ctypes.data, vals.ctypes.data)
+    return bits, vals
