@@ -602,8 +602,8 @@ int vd_synth_device(int options, size_t N, float snr, uint64_t seed, void* bits_
 // ---------------------------------------------------------------- reference-exact channel source
 namespace {
 constexpr uint64_t kMtL = 65536;  // engine outputs per parallel segment
-constexpr int kMtR = 4;           // radix of the jump tree
-constexpr int kMtLevels = 8;      // jump polynomials for trees of up to R^8 = 65536 segments (2^32 outputs)
+constexpr int kMtR = 8;           // radix of the jump tree
+constexpr int kMtLevels = 6;      // jump polynomials for trees of up to R^6 = 262144 segments (2^34 outputs)
 int mt_levels(uint64_t T)
 {
     int k = 0;
@@ -613,7 +613,31 @@ int mt_levels(uint64_t T)
 // segment-start states of std::mt19937(seed) for T segments of kMtL outputs: st[m] = the state after
 // m * kMtL outputs.  Jump tree, top level first: every state at a multiple of R^(k+1) generates its
 // raw words (mt_xseq), then the R-1 children at +c R^k are XOR-accumulated from them (mt_jump).
-int mt_states(uint32_t seed, uint64_t T, uint32_t* st, uint32_t* xs, uint32_t* polys_d, hipStream_t s)
+// jump polynomials on the current device (uploaded once per device, kept for the process)
+int mt_polys_device(const uint32_t** out)
+{
+    static std::mutex mu;
+    static std::vector<uint32_t*> per_dev;
+    int dev = 0;
+    VD_HIP(hipGetDevice(&dev));
+    std::lock_guard<std::mutex> lk(mu);
+    if ((int)per_dev.size() <= dev) per_dev.resize(dev + 1, nullptr);
+    if (!per_dev[dev]) {
+        const std::vector<uint32_t>* polys;
+        try {
+            polys = &vd::mtj::jump_polys(kMtL, kMtR, kMtLevels);
+        } catch (const std::exception& e) {
+            return fail(VD_ERR_DEVICE, std::string("mt19937 jump polynomials: ") + e.what());
+        }
+        uint32_t* p = nullptr;
+        VD_HIP(hipMalloc(&p, polys->size() * 4));
+        VD_HIP(hipMemcpy(p, polys->data(), polys->size() * 4, hipMemcpyHostToDevice));
+        per_dev[dev] = p;
+    }
+    *out = per_dev[dev];
+    return VD_OK;
+}
+int mt_states(uint32_t seed, uint64_t T, uint32_t* st, uint32_t* xs, hipStream_t s)
 {
     using namespace vd::mt;
     VD_HIP(hipMemsetAsync(st, 0, T * kN * 4, s));
@@ -622,21 +646,21 @@ int mt_states(uint32_t seed, uint64_t T, uint32_t* st, uint32_t* xs, uint32_t* p
     const int levels = mt_levels(T);
     if (!levels) return VD_OK;
     if (levels > kMtLevels) return fail(VD_ERR_ARG, "mt19937 stream longer than the jump tree");
-    const std::vector<uint32_t>* polys;
-    try {
-        polys = &vd::mtj::jump_polys(kMtL, kMtR, kMtLevels);  // level k's polynomials do not depend on the depth
-    } catch (const std::exception& e) {
-        return fail(VD_ERR_DEVICE, std::string("mt19937 jump polynomials: ") + e.what());
-    }
-    VD_HIP(hipMemcpyAsync(polys_d, polys->data(), polys->size() * 4, hipMemcpyHostToDevice, s));
+    const uint32_t* polys_d = nullptr;  // level k's polynomials do not depend on the tree depth
+    int rc = mt_polys_device(&polys_d);
+    if (rc) return rc;
     uint64_t step = 1;
     for (int k = 0; k < levels; k++) step *= kMtR;  // R^levels
     for (int k = levels - 1; k >= 0; k--) {
         const uint64_t dstStep = step / kMtR, nsrc = (T + step - 1) / step;
         hipLaunchKernelGGL(mt_xseq, dim3((unsigned)nsrc), dim3(kThreads), 0, s, st, (uint32_t)step, xs);
         VD_HIP(hipGetLastError());
-        hipLaunchKernelGGL(mt_jump, dim3((unsigned)nsrc, kMtR - 1, (kQW + kSliceWords - 1) / kSliceWords), dim3(640), 0,
-                           s, xs, polys_d + (size_t)k * (kMtR - 1) * kQW, (uint32_t)step, (uint32_t)dstStep, (uint32_t)T, st);
+        // slice width: enough workgroups (>= ~4096) on narrow levels, 64 poly words at most
+        const uint64_t jumps = nsrc * (kMtR - 1);
+        int sw = (int)std::min<uint64_t>(kSliceWords, std::max<uint64_t>(4, jumps * kQW / 4096));
+        const unsigned nsl = (unsigned)((kQW + sw - 1) / sw);
+        hipLaunchKernelGGL(mt_jump, dim3((unsigned)nsrc, kMtR - 1, nsl), dim3(64), 0, s, xs,
+                           polys_d + (size_t)k * (kMtR - 1) * kQW, (uint32_t)step, (uint32_t)dstStep, (uint32_t)T, sw, st);
         VD_HIP(hipGetLastError());
         step = dstStep;
     }
@@ -669,31 +693,34 @@ int vd_channel_device(size_t N, float snr, uint32_t bitSeed, uint32_t noiseSeed,
     const uint64_t Tn = (2 * attempts + kMtL - 1) / kMtL;
     const uint64_t Tmax = std::max(Tb, Tn);
     const uint64_t nxs = (Tmax + kMtR - 1) / kMtR;
-    DevBuf stb(s), stn(s), xs(s), pol(s), cnt(s);
+    DevBuf stb(s), stn(s), xs(s), cnt(s);
     VD_HIP(stb.alloc(Tb * kN * 4));
     VD_HIP(xs.alloc(nxs * kNX * 4));
-    VD_HIP(pol.alloc((size_t)kMtLevels * (kMtR - 1) * kQW * 4));
-    int rc = mt_states(bitSeed, Tb, (uint32_t*)stb.p, (uint32_t*)xs.p, (uint32_t*)pol.p, s);
+    int rc = mt_states(bitSeed, Tb, (uint32_t*)stb.p, (uint32_t*)xs.p, s);
     if (rc) return rc;
     hipLaunchKernelGGL(mt_bits, dim3((unsigned)Tb), dim3(kThreads), 0, s, (const uint32_t*)stb.p, kMtL, (uint64_t)N, bits_d);
     VD_HIP(hipGetLastError());
     if (std::isinf(sigma)) {  // AddNoise's stddev = +inf branch (viterbiDF.h:79-85)
-        hipLaunchKernelGGL(mt_noiseless, dim3((unsigned)((nval + 255) / 256)), dim3(256), 0, s, bits_d, nval, values_d);
+        hipLaunchKernelGGL(mt_add_base<false>, dim3((unsigned)((nval + 1023) / 1024)), dim3(256), 0, s,
+                           (const uint8_t*)bits_d, nval, values_d);
         VD_HIP(hipGetLastError());
         return VD_OK;
     }
     VD_HIP(stn.alloc(Tn * kN * 4));
     VD_HIP(cnt.alloc((Tn + 1) * 4));
-    rc = mt_states(noiseSeed, Tn, (uint32_t*)stn.p, (uint32_t*)xs.p, (uint32_t*)pol.p, s);
+    rc = mt_states(noiseSeed, Tn, (uint32_t*)stn.p, (uint32_t*)xs.p, s);
     if (rc) return rc;
     uint32_t* counts = (uint32_t*)cnt.p;
     hipLaunchKernelGGL(mt_noise<0>, dim3((unsigned)Tn), dim3(kThreads), 0, s, (const uint32_t*)stn.p, kMtL, counts,
-                       (const uint8_t*)bits_d, nval, sigma, values_d);
+                       nval, sigma, values_d);
     VD_HIP(hipGetLastError());
     hipLaunchKernelGGL(scan_counts, dim3(1), dim3(1024), 0, s, counts, (uint32_t)Tn);
     VD_HIP(hipGetLastError());
     hipLaunchKernelGGL(mt_noise<1>, dim3((unsigned)Tn), dim3(kThreads), 0, s, (const uint32_t*)stn.p, kMtL, counts,
-                       (const uint8_t*)bits_d, nval, sigma, values_d);
+                       nval, sigma, values_d);
+    VD_HIP(hipGetLastError());
+    hipLaunchKernelGGL(mt_add_base<true>, dim3((unsigned)((nval + 1023) / 1024)), dim3(256), 0, s,
+                       (const uint8_t*)bits_d, nval, values_d);
     VD_HIP(hipGetLastError());
     uint32_t total = 0;
     VD_HIP(hipMemcpyAsync(&total, counts + Tn, 4, hipMemcpyDeviceToHost, s));

@@ -105,37 +105,43 @@ __global__ __launch_bounds__(kThreads) void mt_xseq(const uint32_t* __restrict__
     }
 }
 // jump: st[src + c * dstStep] ^= slice of q_c(A) st[src], for the jump polynomials q_c of one tree
-// level (R - 1 of them, kQW words each).  Grid: (nsrc, R - 1, slices); block = 640 threads, thread j
-// = state word j; each workgroup sums the coefficients [32 * 64 s, 32 * 64 (s + 1)) of its slice.
-constexpr int kSliceWords = 64;  // poly words (of 32 coefficients) per slice
-__global__ __launch_bounds__(640) void mt_jump(const uint32_t* __restrict__ xs, const uint32_t* __restrict__ polys,
-                                               uint32_t srcStep, uint32_t dstStep, uint32_t nstates,
-                                               uint32_t* __restrict__ st)
+// level (R - 1 of them, kQW words each).  Grid: (nsrc, R - 1, slices), one wave per workgroup: lane t
+// accumulates the state words j = t + 64 k (k < 10), so each set coefficient costs one address add,
+// five ds_read2st64_b32 and ten XORs for all 624 words; the coefficient loop is scalar.  A slice is sw
+// poly words (the host picks sw so that narrow tree levels still launch enough workgroups).
+constexpr int kSliceWords = 64;  // largest slice
+__global__ __launch_bounds__(64) void mt_jump(const uint32_t* __restrict__ xs, const uint32_t* __restrict__ polys,
+                                              uint32_t srcStep, uint32_t dstStep, uint32_t nstates, int sw,
+                                              uint32_t* __restrict__ st)
 {
-    __shared__ uint32_t xl[32 * kSliceWords + kN];
-    __shared__ uint32_t ql[kSliceWords];
+    constexpr int NXL = 32 * kSliceWords + 640;
+    __shared__ uint32_t xl[NXL];
     const uint32_t src = blockIdx.x * srcStep, dst = src + (blockIdx.y + 1) * dstStep;
     if (dst >= nstates) return;
-    const int w0 = blockIdx.z * kSliceWords;
-    const int nwq = min(kSliceWords, kQW - w0);
+    const int w0 = blockIdx.z * sw;
+    if (w0 >= kQW) return;
+    const int nwq = min(sw, kQW - w0);
     const uint32_t* x = xs + (size_t)blockIdx.x * kNX + 32 * w0;
-    const int nx = min(32 * kSliceWords + kN, kNX - 32 * w0);
-    for (int i = threadIdx.x; i < nx; i += blockDim.x) xl[i] = x[i];
-    if (threadIdx.x < nwq) ql[threadIdx.x] = polys[(size_t)blockIdx.y * kQW + w0 + threadIdx.x];
+    const int nl = 32 * nwq + 640, nx = min(nl, kNX - 32 * w0);
+    for (int i = threadIdx.x; i < nl; i += 64) xl[i] = i < nx ? x[i] : 0u;
+    const uint32_t* q = polys + (size_t)blockIdx.y * kQW + w0;
     __syncthreads();
-    const int j = threadIdx.x;
-    if (j >= kN) return;
-    uint32_t acc = 0;
+    const int t = threadIdx.x;
+    uint32_t acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     for (int w = 0; w < nwq; w++) {
-        uint32_t bits = __builtin_amdgcn_readfirstlane(ql[w]);
-        const uint32_t* row = xl + 32 * w + j;
+        uint32_t bits = __builtin_amdgcn_readfirstlane(q[w]);
         while (bits) {
             const int b = __builtin_ctz(bits);
             bits &= bits - 1;
-            acc ^= row[b];
+            const uint32_t* row = xl + 32 * w + b + t;
+#pragma unroll
+            for (int k = 0; k < 10; k++) acc[k] ^= row[64 * k];
         }
     }
-    if (acc) atomicXor(st + (size_t)dst * kN + j, acc);
+    uint32_t* o = st + (size_t)dst * kN;
+#pragma unroll
+    for (int k = 0; k < 10; k++)
+        if (t + 64 * k < kN && acc[k]) atomicXor(o + t + 64 * k, acc[k]);
 }
 
 // RandBitGen: bit n = output n >> 31 for n < nbits; segment m = outputs [m L, (m + 1) L)
@@ -162,6 +168,14 @@ __device__ __forceinline__ float canon(uint32_t y)
     const float u = __fmul_rn((float)y, 0x1p-32f);
     return u >= 1.0f ? 0x1.fffffep-1f : u;
 }
+// r2 of a polar attempt (accept: 0 < r2 <= 1)
+__device__ __forceinline__ bool polar_accept(uint32_t o1, uint32_t o2)
+{
+    const float x = __fsub_rn(__fmul_rn(2.0f, canon(o1)), 1.0f);
+    const float y = __fsub_rn(__fmul_rn(2.0f, canon(o2)), 1.0f);
+    const float r2 = __fadd_rn(__fmul_rn(x, x), __fmul_rn(y, y));
+    return !(r2 > 1.0f || r2 == 0.0f);
+}
 // one polar attempt from outputs (u1, u2); returns accepted, and the multiplier m
 __device__ __forceinline__ bool polar(uint32_t o1, uint32_t o2, float& x, float& y, float& m)
 {
@@ -174,31 +188,21 @@ __device__ __forceinline__ bool polar(uint32_t o1, uint32_t o2, float& x, float&
     m = sqrtf(__fdiv_rn(__fmul_rn(-2.0f, glibc_logf(r2)), r2));
     return true;
 }
-// encoded value v (0 .. 2N-1) of the rate-1/2 K=7 (0171, 0133) code, out0 first (viterbiDF.h:36-63)
-__device__ __forceinline__ float base_value(const uint8_t* __restrict__ bits, uint64_t v)
-{
-    const int64_t i = (int64_t)(v >> 1);
-    uint32_t r = 0;  // bit 6 = bit i (newest), bit 0 = bit i-6
-#pragma unroll
-    for (int d = 0; d < 7; d++)
-        if (i - d >= 0) r |= (uint32_t)bits[i - d] << (6 - d);
-    const uint32_t poly = (v & 1) ? 0133u : 0171u;
-    return (__builtin_popcount(r & poly) & 1) ? 1.0f : -1.0f;
-}
-
-// AddNoise.  Attempt a uses outputs 2a, 2a + 1; segment m = attempts [m L/2, (m + 1) L/2).
-// PASS 0 counts the accepted attempts of each segment; PASS 1 (after scan_counts) writes value
-// 2q, 2q + 1 = base + y*m*sigma, base + x*m*sigma of the q-th accepted attempt, q < nvalues / 2.
+// AddNoise's draws.  Attempt a uses outputs 2a, 2a + 1; segment m = attempts [m L/2, (m + 1) L/2).
+// PASS 0 counts the accepted attempts of each segment; PASS 1 (after scan_counts) writes draws
+// 2q, 2q + 1 = y*m*sigma + 0, x*m*sigma + 0 of the q-th accepted attempt, q < nvalues / 2, into
+// values; mt_add_base then adds the BPSK symbols.
 template <int PASS>
 __global__ __launch_bounds__(kThreads) void mt_noise(const uint32_t* __restrict__ st, uint64_t L,
-                                                      uint32_t* __restrict__ counts, const uint8_t* __restrict__ bits,
-                                                      uint64_t nvalues, float sigma, float* __restrict__ values)
+                                                      uint32_t* __restrict__ counts, uint64_t nvalues, float sigma,
+                                                      float* __restrict__ values)
 {
     __shared__ uint32_t buf[2][kN];
     __shared__ uint32_t wsum[kThreads / 64 + 1];
     const uint64_t npairs = nvalues / 2;
     for (int i = threadIdx.x; i < kN; i += kThreads) buf[0][i] = st[(size_t)blockIdx.x * kN + i];
     uint64_t q = PASS ? counts[blockIdx.x] : 0;  // accepted attempts before this segment
+    if (PASS && q >= npairs) return;  // uniform: nothing of this segment is used
     uint32_t cnt = 0;
     __syncthreads();
     int p = 0;
@@ -209,12 +213,13 @@ __global__ __launch_bounds__(kThreads) void mt_noise(const uint32_t* __restrict_
         // 312 attempts per block (pairs of consecutive outputs), two rounds of 256 threads
         for (int r0 = 0; r0 < kN / 2; r0 += kThreads) {
             const int a = r0 + threadIdx.x;
-            bool ok = false;
-            float x = 0.f, y = 0.f, m = 0.f;
-            if (a < kN / 2 && b + 2 * a < L) ok = polar(temper(buf[p][2 * a]), temper(buf[p][2 * a + 1]), x, y, m);
+            const bool in = a < kN / 2 && b + 2 * a < L;
             if constexpr (PASS == 0) {
-                cnt += ok;
+                cnt += in && polar_accept(temper(buf[p][2 * a]), temper(buf[p][2 * a + 1]));
             } else {
+                bool ok = false;
+                float x = 0.f, y = 0.f, m = 0.f;
+                if (in) ok = polar(temper(buf[p][2 * a]), temper(buf[p][2 * a + 1]), x, y, m);
                 const uint64_t bal = __ballot(ok);
                 const uint32_t before = __builtin_popcountll(bal & ((1ull << lane) - 1));
                 if (lane == 0) wsum[wv] = __builtin_popcountll(bal);
@@ -226,10 +231,10 @@ __global__ __launch_bounds__(kThreads) void mt_noise(const uint32_t* __restrict_
                 }
                 const uint64_t qq = q + off + before;
                 if (ok && qq < npairs) {
-                    const float yv = __fadd_rn(__fmul_rn(__fmul_rn(y, m), sigma), 0.0f);
-                    const float xv = __fadd_rn(__fmul_rn(__fmul_rn(x, m), sigma), 0.0f);
-                    values[2 * qq] = __fadd_rn(base_value(bits, 2 * qq), yv);
-                    values[2 * qq + 1] = __fadd_rn(base_value(bits, 2 * qq + 1), xv);
+                    float2 d;
+                    d.x = __fadd_rn(__fmul_rn(__fmul_rn(y, m), sigma), 0.0f);
+                    d.y = __fadd_rn(__fmul_rn(__fmul_rn(x, m), sigma), 0.0f);
+                    *(float2*)(values + 2 * qq) = d;
                 }
                 q += tot;
                 __syncthreads();
@@ -273,11 +278,41 @@ __global__ __launch_bounds__(1024) void scan_counts(uint32_t* counts, uint32_t n
         run += v;
     }
 }
-// stddev = +inf (AddNoise's no-noise branch, viterbiDF.h:79-85): value = base
-__global__ void mt_noiseless(const uint8_t* __restrict__ bits, uint64_t nvalues, float* __restrict__ values)
+// value = base + draw (AddNoise, viterbiDF.h:86-93), or base alone for stddev = +inf (:79-85);
+// 1024 values (512 bits) per workgroup, four per thread
+template <bool NOISE>
+__global__ __launch_bounds__(256) void mt_add_base(const uint8_t* __restrict__ bits, uint64_t nvalues,
+                                                   float* __restrict__ values)
 {
-    const uint64_t v = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (v < nvalues) values[v] = base_value(bits, v);
+    __shared__ uint8_t bl[512 + 8];  // bits i0-8 .. i0+511
+    const uint64_t v0 = (uint64_t)blockIdx.x * 1024, i0 = v0 / 2, nb = nvalues / 2;
+    const int t = threadIdx.x;
+    for (int k = t; k < 520; k += 256) {
+        const int64_t i = (int64_t)i0 - 8 + k;
+        bl[k] = (i >= 0 && (uint64_t)i < nb) ? bits[i] : 0;
+    }
+    __syncthreads();
+    const uint64_t v = v0 + 4 * t;
+    if (v >= nvalues) return;
+    float o[4];
+#pragma unroll
+    for (int e = 0; e < 4; e++) {
+        const int li = (4 * t + e) / 2 + 8;  // bit (v + e) / 2
+        uint32_t r = 0;
+#pragma unroll
+        for (int d = 0; d < 7; d++) r |= (uint32_t)bl[li - d] << (6 - d);
+        o[e] = (__builtin_popcount(r & ((e & 1) ? 0133u : 0171u)) & 1) ? 1.0f : -1.0f;
+    }
+    if (v + 4 <= nvalues) {
+        float4 w = NOISE ? *(const float4*)(values + v) : float4{0.f, 0.f, 0.f, 0.f};
+        w.x = NOISE ? __fadd_rn(o[0], w.x) : o[0];
+        w.y = NOISE ? __fadd_rn(o[1], w.y) : o[1];
+        w.z = NOISE ? __fadd_rn(o[2], w.z) : o[2];
+        w.w = NOISE ? __fadd_rn(o[3], w.w) : o[3];
+        *(float4*)(values + v) = w;
+    } else {
+        for (int e = 0; e < 4 && v + e < nvalues; e++) values[v + e] = NOISE ? __fadd_rn(o[e], values[v + e]) : o[e];
+    }
 }
 
 }  // namespace mt
