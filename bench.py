@@ -98,8 +98,10 @@ def stages_per_launch(opt, input_num):
 
 
 def rank_seed(rank, workload_index):
-    """Seed of the synthetic batch a rank decodes: independent batches per rank (weak scaling)."""
-    return 1000 * rank + workload_index + 1
+    """(bitSeed, noiseSeed) of the batch a rank decodes: independent batches per rank (weak scaling),
+    batch i = 2 rank + workload seeded (1 + 2i, 2 + 2i) as SURVEY 8d's multi-GPU config."""
+    i = 2 * rank + workload_index
+    return (1 + 2 * i, 2 + 2 * i)
 
 
 def aggregate_gbps(bits_per_step, world, steps, elapsed_s):
@@ -159,6 +161,38 @@ def llr_side_measurement(dev, sptr, stream, reps=5):
             "fused_gbps": round(msg / (t_fused * 1e-3) / 1e9, 2), "fused_equals_pack_then_decode": same}
 
 
+def channel_side_measurement(dev, sptr, reps=5, sample_bits=1_000_000):
+    """The reference harness's channel source (RandBitGen | encoder | AddNoise | packer, SOFT8) for one
+    32M-bit batch on the GPU (vd_simulate_device), against the host harness (libstdc++ generators, one
+    thread) on a 1M-bit sample with the same seeds, checked equal.  Outside the timed region."""
+    opt = vitdec.SOFT8 | vitdec.M_B16
+    bits = torch.empty(N_BITS, dtype=torch.uint8, device=dev)
+    packed = torch.empty(vitdec.lib().vd_input_size(opt, 2 * N_BITS), dtype=torch.uint8, device=dev)
+    run = lambda n: vitdec.simulate_device(opt, n, SNR_DB, 7, 8, bits.data_ptr(), packed.data_ptr(), sptr)
+    run(N_BITS)
+    ts = []
+    for _ in range(reps):
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        run(N_BITS)
+        torch.cuda.synchronize()
+        ts.append(time.perf_counter() - t)
+    t_dev = sorted(ts)[len(ts) // 2]
+    t = time.perf_counter()
+    hb, hp = vitdec.simulate_host(opt, sample_bits, SNR_DB, 7, 8)
+    t_host = time.perf_counter() - t
+    run(sample_bits)
+    torch.cuda.synchronize()
+    nb = hp.nbytes
+    same = bool(np.array_equal(packed[:nb].cpu().numpy(), hp.view(np.uint8)) and
+                np.array_equal(bits[:sample_bits].cpu().numpy(), hb))
+    return {"workload": "32M-bit SOFT8 batch from seeds (7, 8)", "device_ms": round(t_dev * 1e3, 3),
+            "device_gbit_per_s": round(N_BITS / t_dev / 1e9, 2),
+            "host_harness": {"sample_bits": sample_bits, "ms": round(t_host * 1e3, 1),
+                             "mbit_per_s": round(sample_bits / t_host / 1e6, 2), "threads": 1},
+            "device_equals_host_on_sample": same}
+
+
 def pcie_side_measurement(batches, dev, nb=6):
     """PCIe-inclusive rate (the reference run()'s scope: host buffers in, host buffers out): nb
     independent batches per workload in pinned host memory through vd_run_stream, which decodes them
@@ -190,6 +224,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-llr", action="store_true", help="skip the float-input (packer fused) side measurement")
     ap.add_argument("--no-pcie", action="store_true", help="skip the host-to-host pipelined side measurement")
+    ap.add_argument("--no-channel", action="store_true", help="skip the channel-source side measurement")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -213,7 +248,10 @@ def main():
         inp = torch.empty(nin, dtype=torch.uint8, device=dev)
         bits = torch.empty(N_BITS, dtype=torch.uint8, device=dev)
         out = torch.empty(nout, dtype=torch.uint8, device=dev)
-        vitdec.synth_device(opt, N_BITS, SNR_DB, rank_seed(rank, wi), bits.data_ptr(), inp.data_ptr(), sptr)
+        # the reference harness's own chain (std::mt19937 bits and noise, BPSK+AWGN, quantiser at 40000),
+        # generated bit-exactly on the GPU (vd_simulate_device)
+        bs, ns = rank_seed(rank, wi)
+        vitdec.simulate_device(opt, N_BITS, SNR_DB, bs, ns, bits.data_ptr(), inp.data_ptr(), sptr)
         dec = vitdec.ViterbiCUDA(opt, 0, dev)
         batches.append(dict(name=name, opt=opt, input_num=input_num, inp=inp, out=out, bits=bits, dec=dec,
                             msg=vitdec.lib().vd_message_len(opt, input_num)))
@@ -258,6 +296,7 @@ def main():
         sums.append(int(np.bitwise_xor.reduce(out_h.view(np.uint32))))
     llr = None if args.no_llr else llr_side_measurement(dev, sptr, stream)
     pcie = None if args.no_pcie else pcie_side_measurement(batches, dev)
+    chan = None if (args.no_channel or rank != 0) else channel_side_measurement(dev, sptr)
     if world > 1:
         elapsed = max_over_ranks(elapsed, dev)
         gathered = gather_checksums(sums, dev, world)
@@ -296,8 +335,9 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "int32+int16x2",
-            "data": f"synthetic: GPU counter-hash bits, K=7 (0171,0133) encoder, BPSK+AWGN at {SNR_DB} dB, "
-                    f"quantiser scale 40000 (reference harness scaling)",
+            "data": f"synthetic: the reference harness chain generated on the GPU bit-exactly (std::mt19937 "
+                    f"bits, K=7 (0171,0133) encoder, BPSK + normal_distribution<float> AWGN at {SNR_DB} dB, "
+                    f"quantiser scale 40000), seeds (1+2i, 2+2i) for batch i = 2 rank + workload",
             "config": {
                 "workload": "per GPU per step: one 32M-bit HARD batch on the int32 core + one 32M-bit SOFT8 "
                             "batch on the int16x2 core (BASELINE configs[1]+[2]); each batch uses the "
@@ -328,6 +368,8 @@ def main():
             result["config"]["llr_input"] = llr
         if pcie is not None:
             result["config"]["pcie_inclusive"] = pcie
+        if chan is not None:
+            result["config"]["channel_source"] = chan
         if not args.no_cpu_baseline and world == 1:
             result["cpu_baseline"] = cpu_baseline(batches)
         print(json.dumps(result), flush=True)

@@ -6,7 +6,7 @@ export TMPDIR=/tmp
 TAG=${1:-pmc}
 O=gpurun_out/$TAG
 mkdir -p $O
-B="python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-llr --no-pcie"
+B="python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-llr --no-pcie --no-channel"
 run() { timeout -s KILL 120 rocprofv3 --pmc $1 -d $O/$2 -o run --output-format csv -- $B > $O/$2.log 2>&1; }
 run "FETCH_SIZE" fetch && \
 run "WRITE_SIZE" write && \

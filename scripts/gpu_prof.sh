@@ -9,7 +9,7 @@ O=gpurun_out/$TAG
 mkdir -p $O
 timeout -k 10 300 python bench.py > $O/bench.log 2>&1 || { echo bench failed; tail -20 $O/bench.log; exit 1; }
 tail -1 $O/bench.log
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof -o run --output-format csv -- python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-llr --no-pcie > $O/prof.log 2>&1 || { echo prof failed; tail -20 $O/prof.log; exit 1; }
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof -o run --output-format csv -- python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-llr --no-pcie --no-channel > $O/prof.log 2>&1 || { echo prof failed; tail -20 $O/prof.log; exit 1; }
 find $O/prof -name "*kernel_stats.csv" -exec cp {} $O/kernel_stats.csv \;
 tail -1 $O/prof.log
 head -5 $O/kernel_stats.csv
