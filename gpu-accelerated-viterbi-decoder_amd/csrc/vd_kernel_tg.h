@@ -110,21 +110,42 @@ __device__ __forceinline__ void tg_stage_dpp(float& V, float m)
 // v_pk_fma_f32, swap halves across lanes, max.  The butterfly partner has the same label in both swap
 // phases, so m' = m except in M_B32's phase-0 rows (m, m' = the two tag signs).  SEL picks the halves of
 // the table pair e: 0 = (lo, lo) (even period), 1 = (hi, hi) (odd period), 2 = (lo, hi) (M_B32 phase 0).
-template <int Q, int SEL>
+// VAR (tools only, timing studies; results wrong): 1 no lane swap, 2 s_nop 0, 4 swap + max only
+template <int Q, int SEL, int VAR = 0>
 __device__ __forceinline__ void tg_stage_swap(float& V, f2v e, f2v s)
 {
-#define VD_TG_SWAP(SW, OS)                                                                            \
-    asm("v_pk_fma_f32 v[62:63], %1, %2, v[60:61] " OS "\n\ts_nop 1\n\t" SW " v62, v63\n\t"             \
-        "v_max_f32 %0, v62, v63"                                                                      \
-        : "+{v60}"(V) : "v"(e), "v"(s) : "v62", "v63")
-#define VD_TG_SWAP_SEL(SW)                                                                            \
-    if constexpr (SEL == 0) VD_TG_SWAP(SW, "op_sel:[0,0,0] op_sel_hi:[0,1,0]");                      \
-    else if constexpr (SEL == 1) VD_TG_SWAP(SW, "op_sel:[1,0,0] op_sel_hi:[1,1,0]");                 \
-    else VD_TG_SWAP(SW, "op_sel:[0,0,0] op_sel_hi:[1,1,0]");
+#define VD_TG_ASM(PK, NOP, SWP) \
+    asm(PK NOP SWP "v_max_f32 %0, v62, v63" : "+{v60}"(V) : "v"(e), "v"(s) : "v62", "v63")
+#define VD_TG_SWAP(SW, OS)                                                                                  \
+    if constexpr (VAR == 0) VD_TG_ASM("v_pk_fma_f32 v[62:63], %1, %2, v[60:61] " OS "\n\t", "s_nop 1\n\t", SW " v62, v63\n\t"); \
+    else if constexpr (VAR == 1) VD_TG_ASM("v_pk_fma_f32 v[62:63], %1, %2, v[60:61] " OS "\n\t", "s_nop 1\n\t", "");              \
+    else if constexpr (VAR == 2) VD_TG_ASM("v_pk_fma_f32 v[62:63], %1, %2, v[60:61] " OS "\n\t", "s_nop 0\n\t", SW " v62, v63\n\t"); \
+    else VD_TG_ASM("", "s_nop 1\n\t", SW " v62, v63\n\t");
+#define VD_TG_SWAP_SEL(SW)                                                                                  \
+    if constexpr (SEL == 0) { VD_TG_SWAP(SW, "op_sel:[0,0,0] op_sel_hi:[0,1,0]") }                           \
+    else if constexpr (SEL == 1) { VD_TG_SWAP(SW, "op_sel:[1,0,0] op_sel_hi:[1,1,0]") }                      \
+    else { VD_TG_SWAP(SW, "op_sel:[0,0,0] op_sel_hi:[1,1,0]") }
     if constexpr (Q == 4) { VD_TG_SWAP_SEL("v_permlane16_swap_b32") }
     else { VD_TG_SWAP_SEL("v_permlane32_swap_b32") }
 #undef VD_TG_SWAP_SEL
 #undef VD_TG_SWAP
+#undef VD_TG_ASM
+}
+
+// swap stage with the partner's metric fetched through the LDS crossbar (ds_bpermute, no memory access)
+// instead of a VALU lane swap: V' = max(V + m, V_partner - m), the DPP stage's formula, with m the
+// entry of this lane's class (M_B32 phase 0: E- in the lower position half, E+ in the upper one).
+__device__ __forceinline__ float tg_partner(float V, int paddr)
+{
+    return __builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute(paddr, __builtin_bit_cast(int, V)));
+}
+template <int SEL>
+__device__ __forceinline__ void tg_stage_lds(float& V, f2v e, float vp, bool upper)
+{
+    const float m = SEL == 0 ? e.x : SEL == 1 ? e.y : (upper ? e.y : e.x);
+    float t1, t2;
+    asm("v_add_f32 %1, %0, %3\n\tv_sub_f32 %2, %4, %3\n\tv_max_f32 %0, %1, %2"
+        : "+{v60}"(V), "=&v"(t1), "=&v"(t2) : "v"(m), "v"(vp));
 }
 
 // ---------------------------------------------------------------- group traceback (reference viterbiTB.cuh:4-21)
@@ -340,6 +361,8 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(7))
         constexpr int K = decltype(KK)::value;
         aK[K] = 8 * own_label(pos, K);
     });
+    const int pa5 = 4 * (lane ^ 32);  // ds_bpermute address of the xor-32 partner (tools variant)
+    const bool upper5 = (pos >> 5) & 1;
     f2v sxp[2];
     sfor<2>([&](auto W) {
         constexpr int w = decltype(W)::value;  // 0: K=0 (Q=5), 1: K=5 (Q=4)
@@ -404,12 +427,23 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(7))
             // ABL (tools only): 2 = no table reads, 128 = every stage a DPP stage, 4 = no field read-out
             constexpr bool ODD = (r / 6) % 2 == 1;
             constexpr int RP = TT::pairrow(K) ? r : (ODD ? r - 6 : r);  // where this stage's pair was read
+            // Q=4 (lane xor 16) fetches the partner's metric through the LDS crossbar (ds_swizzle), Q=5
+            // (xor 32) swaps candidates with v_permlane32_swap: a VALU lane swap costs two issue slots, the
+            // swizzle none, and doing both through the LDS queues them behind each other and the table
+            // reads (tools/vd_swapab).  ABL (tools only): 16384 = Q=4 by v_permlane16_swap too,
+            // 8192 = Q=5 by ds_bpermute.
+            constexpr bool LSW = (Q == 5 && (ABL & 8192)) || (Q == 4 && !(ABL & 16384));
             if constexpr (Q <= 3 || (ABL & 128)) {
                 const float m = (ABL & 2) ? (float)aK[K] : (ODD ? vp[RP].y : vp[RP].x);
                 tg_stage_dpp<(Q <= 3 ? Q : 3)>(V, m);
+            } else if constexpr (LSW) {
+                const float pv = Q == 4 ? __builtin_bit_cast(float, __builtin_amdgcn_ds_swizzle(__builtin_bit_cast(int, V), 0x401F))
+                                        : tg_partner(V, pa5);
+                const f2v e = (ABL & 2) ? (f2v){(float)aK[K], 1.0f} : vp[RP];
+                tg_stage_lds<TT::pairrow(K) ? 2 : (ODD ? 1 : 0)>(V, e, pv, upper5);
             } else {
                 const f2v e = (ABL & 2) ? (f2v){(float)aK[K], 1.0f} : vp[RP];
-                tg_stage_swap<Q, TT::pairrow(K) ? 2 : (ODD ? 1 : 0)>(V, e, sxp[K == 0 ? 0 : 1]);
+                tg_stage_swap<Q, TT::pairrow(K) ? 2 : (ODD ? 1 : 0), (ABL >> 10) & 7>(V, e, sxp[K == 0 ? 0 : 1]);
             }
             if constexpr (r + TGD < 96) issue(std::integral_constant<int, r + TGD>{});
             if constexpr (i % J == J - 1 && !(ABL & 4)) {

@@ -1,0 +1,51 @@
+// vd_swapab.hip -- timing-only study of the tagged kernel's swap stages (ABL bits 1024.. select
+// tg_stage_swap variants; outputs of ABL != 0 are wrong), interleaved in one process.
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+#include <algorithm>
+#include "../gpu-accelerated-viterbi-decoder_amd/csrc/vd_kernel_tg.h"
+#define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP error %s at %d\n", hipGetErrorString(e), __LINE__); exit(1); } } while (0)
+using KFn = void (*)(const void*, void*, vd::Geom);
+struct Var { const char* name; KFn fn; };
+template <int ABL> Var hb(const char* n) { return {n, (KFn)vd::vd_decode_tg<vd::HARD, vd::B32, 32, ABL>}; }
+int main(int argc, char** argv)
+{
+    const size_t N = 32000000, inBytes = 2 * N * 4;
+    void *in, *out;
+    CK(hipMalloc(&in, inBytes));
+    CK(hipMalloc(&out, 16u << 20));
+    std::vector<uint32_t> h(inBytes / 4);
+    uint32_t x = 12345;
+    for (auto& w : h) { x ^= x << 13; x ^= x >> 17; x ^= x << 5; w = x; }
+    CK(hipMemcpy(in, h.data(), inBytes, hipMemcpyHostToDevice));
+    vd::Geom g;
+    g.packNum = (N - 64) / 32;
+    g.nchunks = 6400;
+    g.availStages = N;
+    g.scale = 1.0f;
+    CK(hipMalloc(&g.fair, vd::kFairSlots * 8));
+    CK(hipMemset(g.fair, 0, vd::kFairSlots * 8));
+    std::vector<Var> v = {hb<0>("full (Q4 swizzle)"), hb<16384>("Q4 permlane16 (previous)"), hb<8192>("Q4 swizzle + Q5 bpermute"),
+                          hb<128>("all-dpp"), hb<16384 | 1024>("swaps without lane movement"),
+                          hb<1 | 2 | 4 | 8 | 16>("ACS only"), hb<1 | 2 | 4 | 8 | 16 | 128>("ACS only all-dpp")};
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
+    const int rounds = argc > 1 ? atoi(argv[1]) : 10;
+    std::vector<std::vector<float>> t(v.size());
+    for (int r = 0; r < rounds + 2; r++)
+        for (size_t i = 0; i < v.size(); i++) {
+            CK(hipEventRecord(e0));
+            hipLaunchKernelGGL(v[i].fn, dim3(1600), dim3(256), 0, 0, in, out, g);
+            CK(hipEventRecord(e1));
+            CK(hipEventSynchronize(e1));
+            float ms; CK(hipEventElapsedTime(&ms, e0, e1));
+            if (r >= 2) t[i].push_back(ms);
+        }
+    for (size_t i = 0; i < v.size(); i++) {
+        std::sort(t[i].begin(), t[i].end());
+        printf("%-28s median %.4f ms  min %.4f ms\n", v[i].name, t[i][t[i].size() / 2], t[i][0]);
+    }
+    return 0;
+}
