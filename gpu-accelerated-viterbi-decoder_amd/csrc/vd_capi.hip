@@ -7,6 +7,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
+#include <cstdlib>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -96,6 +98,13 @@ uint64_t avail_stages(int o, size_t n)
 
 using launch_fn = void (*)(const void*, void*, vd::Geom, hipStream_t);
 
+// workgroups of a tagged-kernel launch: kWaves whole chunks each, plus one per split chunk
+unsigned tg_grid(const vd::Geom& g)
+{
+    if (g.nwhole == 0) return (g.nchunks + vd::kWaves - 1) / vd::kWaves;
+    return g.nwhole / vd::kWaves + (g.nchunks - g.nwhole);
+}
+
 template <int CH, int CORE, int OB>
 void launch_t(const void* in, void* out, vd::Geom g, hipStream_t s)
 {
@@ -104,8 +113,7 @@ void launch_t(const void* in, void* out, vd::Geom g, hipStream_t s)
         hipLaunchKernelGGL((vd::vd_decode_sc<CH, CORE, OB>), dim3((g.nchunks + vd::kWaves - 1) / vd::kWaves),
                            dim3(64 * vd::kWaves), 0, s, in, out, g);
     else
-        hipLaunchKernelGGL((vd::vd_decode_tg<CH, CORE, OB>), dim3((g.nchunks + vd::kWaves - 1) / vd::kWaves),
-                           dim3(64 * vd::kWaves), 0, s, in, out, g);
+        hipLaunchKernelGGL((vd::vd_decode_tg<CH, CORE, OB>), dim3(tg_grid(g)), dim3(64 * vd::kWaves), 0, s, in, out, g);
 }
 
 template <int CH, int CORE>
@@ -131,8 +139,8 @@ launch_fn pick(int o)
 template <int CH, int CORE, int OB>
 void launch_llr_t(const void* in, void* out, vd::Geom g, hipStream_t s)
 {
-    hipLaunchKernelGGL((vd::vd_decode_tg<vd::kLlr + CH, CORE, OB>), dim3((g.nchunks + vd::kWaves - 1) / vd::kWaves),
-                       dim3(64 * vd::kWaves), 0, s, in, out, g);
+    hipLaunchKernelGGL((vd::vd_decode_tg<vd::kLlr + CH, CORE, OB>), dim3(tg_grid(g)), dim3(64 * vd::kWaves), 0, s, in,
+                       out, g);
 }
 template <int CH, int CORE>
 launch_fn pick_llr_ob(int ob)
@@ -237,6 +245,63 @@ static unsigned long long* fair_board(int device)
     return boards[device];
 }
 
+// Per-device bookkeeping of split launches (vd_kernel_tg.h "split chunks"): kSplitSlots slots, a launch
+// uses slot epoch % kSplitSlots, so up to that many split launches may be in flight on a device at once.
+constexpr int kSplitSlots = 16;
+struct SplitState {
+    int nsimd = 0;
+    uint32_t maxSplit = 0;      // split chunks a slot holds
+    float* spec = nullptr;      // [slot][maxSplit][kWaves][64]
+    uint32_t* flags = nullptr;  // [slot][maxSplit][16]
+    uint32_t* stats = nullptr;  // re-decoded split chunks (all launches)
+    std::atomic<uint32_t> epoch{0};
+};
+static SplitState* split_state(int device)
+{
+    static std::mutex mu;
+    static std::vector<SplitState*> st;
+    std::lock_guard<std::mutex> lk(mu);
+    if ((int)st.size() <= device) st.resize(device + 1, nullptr);
+    if (!st[device]) {
+        int cus = 0;
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus <= 0)
+            return nullptr;
+        SplitState* x = new SplitState;
+        x->nsimd = 4 * cus;
+        x->maxSplit = (uint32_t)(x->nsimd / vd::kWaves);
+        const size_t nspec = (size_t)kSplitSlots * x->maxSplit * vd::kWaves * 64, nflag = (size_t)kSplitSlots * x->maxSplit * 16;
+        if (hipMalloc(&x->spec, nspec * 4) != hipSuccess || hipMalloc(&x->flags, (nflag + 1) * 4) != hipSuccess ||
+            hipMemset(x->flags, 0, (nflag + 1) * 4) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
+            delete x;
+            return nullptr;
+        }
+        x->stats = x->flags + nflag;
+        st[device] = x;
+    }
+    return st[device];
+}
+// split the launch when the chunks leave a remainder of exactly one piece wave per SIMD (6400 chunks
+// on 1024 SIMDs: 6 whole chunks per SIMD + 256 chunks in 4 pieces) and the chunks are long enough
+static void plan_split(vd::Geom& g, int options, int device)
+{
+    if (out_of(options) != 0 || ch_of(options) == vd::SOFT16) return;  // O_B32, tagged kernel only
+    if (const char* e = std::getenv("VD_NO_SPLIT"))
+        if (e[0] == '1') return;
+    SplitState* x = split_state(device);
+    if (!x) return;
+    const uint32_t perSimd = g.nchunks / (uint32_t)x->nsimd, rem = g.nchunks % (uint32_t)x->nsimd;
+    if (rem == 0 || rem * vd::kWaves != (uint32_t)x->nsimd || perSimd + 1 > 7) return;
+    if (g.packNum / g.nchunks < (uint64_t)vd::kSplitMinWords) return;
+    uint32_t e = x->epoch.fetch_add(1) + 1;
+    if (e == 0) e = x->epoch.fetch_add(1) + 1;  // 0 marks "never set"
+    const uint32_t slot = e % kSplitSlots;
+    g.nwhole = g.nchunks - rem;
+    g.epoch = e;
+    g.spec = x->spec + (size_t)slot * x->maxSplit * vd::kWaves * 64;
+    g.flags = x->flags + (size_t)slot * x->maxSplit * 16;
+    g.stats = x->stats;
+}
+
 // llr: in_d holds inputNum float channel values, quantised in the kernel (scale = packer scale)
 static int launch_decode(int options, const void* in_d, void* out_d, size_t inputNum, hipStream_t s,
                          bool llr = false, float scale = 1.0f)
@@ -254,6 +319,7 @@ static int launch_decode(int options, const void* in_d, void* out_d, size_t inpu
     VD_HIP(hipGetDevice(&dev));
     g.fair = fair_board(dev);
     if (!g.fair) return fail(VD_ERR_NOMEM, "progress board allocation failed");
+    plan_split(g, options, dev);
     f(in_d, out_d, g, s);
     VD_HIP(hipGetLastError());
     return VD_OK;
@@ -266,6 +332,17 @@ size_t vd_input_size(int options, size_t n) { return input_size(options, n); }
 size_t vd_message_len(int options, size_t n) { return message_len(options, n); }
 size_t vd_output_size(int options, size_t n) { return message_len(options, n) / 8; }
 int vd_num_chunks(void) { return vd::kChunks; }
+
+int vd_split_redecodes(int device, uint64_t* count)
+{
+    if (!count) return fail(VD_ERR_ARG, "null argument");
+    SplitState* x = split_state(device);
+    if (!x) return fail(VD_ERR_DEVICE, "split bookkeeping unavailable");
+    uint32_t v = 0;
+    VD_HIP(hipMemcpy(&v, x->stats, 4, hipMemcpyDeviceToHost));
+    *count = v;
+    return VD_OK;
+}
 const char* vd_last_error(void) { return g_err.c_str(); }
 const char* vd_kernel_name(int options) { return kname(options); }
 

@@ -330,6 +330,88 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t tg_rsrc(const void* in, uint64
                                              (int)(uint32_t)(rem < 0xFFFFFFFFull ? rem : 0xFFFFFFFFull), 0x00020000);
 }
 
+// ---------------------------------------------------------------- split chunks
+// A launch of 6400 chunks on 1024 SIMDs puts 7 waves on a quarter of the SIMDs and 6 on the rest; the
+// 7-wave SIMDs set the kernel time.  In a split launch (Geom::nwhole) the first nwhole chunks are
+// decoded whole, one per wave, and each remaining chunk by one workgroup as kWaves pieces, so every
+// SIMD gets 6 whole chunks and one piece.  Piece 0 starts at the chunk start (exact).  Piece q > 0
+// starts kSplitWarm blocks before its first word's emit block from equal metrics and publishes its
+// renormalised metric vector at that block (split_publish); piece q-1 compares its own vector at the
+// same block (split_check).  Equal vectors mean every later decision of piece q equals the exact
+// decode's (the recursion and the tie rules depend only on metric differences; V at a block start is
+// VBASE + (metric - metric of position 0) * 2^S with cleared fields).  Piece 0 accepts pieces in order
+// while the checks passed (split_commit); otherwise it stops the pieces' output (cancel flag) and
+// re-decodes the whole chunk.  Block boundaries are multiples of 3 (the group length, 96 stages = 16
+// trellis periods) so both runs use the same position <-> state map there.  Flags carry the launch
+// epoch, so nothing is reset between launches; every wait is bounded (timeout = re-decode).  The
+// pieces of a chunk are the waves of one workgroup (one CU), so every flag and fence is workgroup-
+// scoped: an agent-scope release would write back the XCD's L2 at each flag.
+// flags[16] per split chunk: [q] spec ready (epoch), [4+q] check of boundary q (2 epoch + ok),
+// [8+q] piece q done (epoch), [12] cancel (epoch).
+constexpr int kSplitWarm = 6;      // warm-up blocks of a speculative piece (multiple of 3)
+constexpr int kSplitMinWords = 64; // chunks shorter than this are not split (host side)
+struct SplitGeo {
+    uint32_t s0, words, E;
+    int Xspec, Xcmp;
+};
+// boundary word of piece q (q = 1 .. kWaves-1): (k + 1) % 3 == 0, so the boundary block k + 1 starts a group
+__device__ __forceinline__ uint32_t split_bound(uint32_t Sc, int q)
+{
+    const uint32_t k = (uint32_t)q * Sc / kWaves;
+    return k - (k + 1) % 3;
+}
+__device__ __forceinline__ SplitGeo split_geo(uint32_t Sc, int q)
+{
+    SplitGeo g;
+    const uint32_t kq = q == 0 ? 0 : split_bound(Sc, q);
+    const uint32_t kn = q == kWaves - 1 ? Sc : split_bound(Sc, q + 1);
+    g.s0 = q == 0 ? 0 : kq + 1 - kSplitWarm;
+    g.words = kn - g.s0;
+    g.E = kq - g.s0;
+    g.Xspec = q == 0 ? -1 : (int)(kq + 1 - g.s0);
+    g.Xcmp = q == kWaves - 1 ? -1 : (int)(kn + 1 - g.s0);
+    return g;
+}
+__device__ __forceinline__ void split_publish(uint32_t* flags, float* spec, int q, float V, int lane, uint32_t epoch)
+{
+    spec[q * 64 + lane] = V;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    if (lane == 0) __hip_atomic_store(flags + q, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ bool split_check(uint32_t* flags, const float* spec, int q, float V, int lane, uint32_t epoch)
+{
+    const uint32_t f = __builtin_amdgcn_readfirstlane(
+        __hip_atomic_load(flags + q, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
+    if (f != epoch) return false;  // not published yet: treated as a mismatch
+    const float sv = __hip_atomic_load(spec + q * 64 + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    return __ballot(__builtin_bit_cast(uint32_t, sv) != __builtin_bit_cast(uint32_t, V)) == 0;
+}
+__device__ __forceinline__ void split_finish(uint32_t* flags, int q, bool cmpOk, int lane, uint32_t epoch)
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");  // this piece's output words before its flags
+    if (lane == 0) {
+        if (q + 1 < kWaves) __hip_atomic_store(flags + 4 + q + 1, 2 * epoch + (cmpOk ? 1u : 0u), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        __hip_atomic_store(flags + 8 + q, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+}
+// piece 0, after its own words: true iff every piece's start checked equal (waits, bounded, for the
+// pieces to finish: they run kSplitWarm blocks longer than piece 0)
+__device__ __forceinline__ bool split_commit(uint32_t* flags, bool cmp1, uint32_t epoch)
+{
+    if (!cmp1) return false;
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();  // 100 MHz
+    for (int q = 1; q < kWaves; q++) {
+        while (__builtin_amdgcn_readfirstlane(__hip_atomic_load(flags + 8 + q, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)) != epoch) {
+            if (__builtin_amdgcn_s_memrealtime() - t0 > 200000) return false;  // 2 ms: give up, re-decode
+            __builtin_amdgcn_s_sleep(4);
+        }
+        if (q + 1 < kWaves &&
+            __builtin_amdgcn_readfirstlane(__hip_atomic_load(flags + 4 + q + 1, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)) != 2 * epoch + 1)
+            return false;
+    }
+    return true;
+}
+
 // ================================================================ tagged kernel: one chunk per wave
 template <int CH, int CORE, int OB, int ABL = 0>
 __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(7))) void vd_decode_tg(const void* __restrict__ in, void* __restrict__ out, Geom geo)
@@ -345,13 +427,18 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(7))
     const int pos = tg_pos(lane);
     char* tabb = tab_all[wv];
     uint32_t* ring = ring_all[wv];
-    const ChunkRange cr = chunk_range(geo, blockIdx.x * kWaves + wv);
+    // This wave's work: chunk blockIdx.x * kWaves + wv, or, in a split launch (Geom::nwhole), piece wv of
+    // chunk nwhole + (blockIdx.x - nwhole / kWaves) -- see "split chunks" at the end of the file.
+    const bool split = OB == 32 && geo.nwhole != 0 && blockIdx.x >= geo.nwhole / kWaves;
+    const uint32_t chunk = split ? geo.nwhole + (blockIdx.x - geo.nwhole / kWaves) : blockIdx.x * kWaves + wv;
+    const int piece = split ? wv : -1;
+    const ChunkRange cr = chunk_range(geo, chunk);
     if (cr.words == 0) return;
     const uint64_t t_clk0 = (ABL & 32) ? __builtin_amdgcn_s_memtime() : 0;
     const uint64_t t_rt0 = (ABL & 32) ? __builtin_amdgcn_s_memrealtime() : 0;
-    const uint64_t start = cr.startWord * OB;
-    const uint32_t Sw = OB == 32 ? cr.words : (cr.words + 1) / 2;  // 32-bit words traced back
-    const uint32_t nblk = Sw + 2;
+    const uint32_t Sc = OB == 32 ? cr.words : (cr.words + 1) / 2;  // 32-bit words traced back (chunk)
+    uint32_t* const sflags = split ? geo.flags + (size_t)(chunk - geo.nwhole) * 16 : nullptr;
+    float* const sspec = split ? geo.spec + (size_t)(chunk - geo.nwhole) * kWaves * 64 : nullptr;
 
     // per-lane LDS byte addresses of this position's table entries (row offsets are compile-time)
     // per-lane LDS byte offset of this position's entry in a phase-K row (row offsets are compile-time);
@@ -380,9 +467,7 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(7))
     // bits: V = 1.5*2^23 + metric*2^S + 2^(S-1) + h.  The 2^(S-1) offset keeps the history field
     // 2^(S-1) + h in (0, 2^S), so read-out and clearing are bit operations on the pattern.
     constexpr uint32_t VBASE = 0x4B400000u + (1u << (S - 1));  // pattern of 1.5*2^23 + 2^(S-1)
-    float V = __builtin_bit_cast(float, VBASE);
     const uint32_t fnm = ~((1u << S) - 1u), fhf = 1u << (S - 1);  // field clear: (p & fnm) | fhf
-    uint32_t kb = 0;
     unsigned long long* fb = nullptr;
     unsigned long long fret = 0;
     uint32_t fadded = 0;
@@ -392,9 +477,28 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(7))
             if (lane == 0) atomicAdd(fb, 1ull << 32);
         }
     }
-    uint32_t tbn = TBS - 3 * (blockIdx.x & 3);
     const uint64_t availB = IN::bytes(geo.availStages);
     const uint32_t vo1 = IN::voff(lane), vo2 = IN::voff((int)li);
+    for (int pass = 0;; pass++) {
+    // the words of this pass: [s0, s0 + Sw) of the chunk, written from word s0 + E on; Xspec / Xcmp:
+    // group-start blocks where a piece publishes / checks a metric vector (-1: none)
+    uint32_t s0 = 0, Sw = Sc, E = 0;
+    int Xspec = -1, Xcmp = -1;
+    if (piece >= 0 && pass == 0) {
+        const SplitGeo sg = split_geo(Sc, piece);
+        s0 = sg.s0;
+        Sw = sg.words;
+        E = sg.E;
+        Xspec = sg.Xspec;
+        Xcmp = sg.Xcmp;
+    }
+    const uint64_t wOut = cr.startWord + s0;  // output word of local word 0 (OB == 32 when split)
+    const uint64_t start = wOut * OB;
+    const uint32_t nblk = Sw + 2;
+    bool cmpOk = false;
+    float V = __builtin_bit_cast(float, VBASE);
+    uint32_t kb = 0;
+    uint32_t tbn = TBS - 3 * (blockIdx.x & 3);
     __amdgpu_buffer_rsrc_t rs = tg_rsrc<CH>(in, start, availB);
     typename IN::raw_t rA = IN::template load<0>(rs, vo1);  // stage `lane` of the group
     typename IN::raw_t rB = IN::template load<2>(rs, vo2);  // stage 64 + li
@@ -471,12 +575,15 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(7))
         if (j >= 2 && (j - 1 - kb == tbn || j == nblk - 1)) {
             wave_sync();
             const uint32_t nw = j - 1 - kb;
-            if (!(ABL & 1) && (uint32_t)lane < nw) {
+            // a speculative piece stops writing once its chunk is being re-decoded (cancel flag)
+            const bool cancelled = piece > 0 && pass == 0 &&
+                                   __hip_atomic_load(sflags + 12, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == geo.epoch;
+            if (!(ABL & 1) && (uint32_t)lane < nw && kb + lane >= E && !cancelled) {
                 const uint64_t k = kb + lane;
                 const uint32_t Q0 = (uint32_t)(wv * (TBS + 1) * 256 + (lane + 1) * 256);
                 uint32_t w = traceback_word_tg<J, CORE == B32>((const char*)ring_all, Q0, k);
                 if constexpr (OB == 32) {
-                    ((uint32_t*)out)[cr.startWord + k] = w;
+                    ((uint32_t*)out)[wOut + k] = w;
                 } else {
                     uint16_t* o = (uint16_t*)out + cr.startWord;
                     o[2 * k] = (uint16_t)(w >> 16);
@@ -550,6 +657,8 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(7))
                 fadded += 3;
             }
         }
+        if (split && (int)j == Xspec) split_publish(sflags, sspec, piece, V, lane, geo.epoch);
+        if (split && (int)j == Xcmp) cmpOk = split_check(sflags, sspec, piece + 1, V, lane, geo.epoch);
         wave_sync();
         sfor<TGD>([&](auto X) { issue(X); });
         if (!block(std::integral_constant<int, 0>{}, j)) break;
@@ -557,6 +666,18 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(7))
         if (!block(std::integral_constant<int, 4>{}, j + 2)) break;
         wave_sync();
     }
+    if (piece < 0 || pass > 0) break;
+    if (piece > 0) {  // speculative piece: record the check of the next boundary, then done
+        split_finish(sflags, piece, cmpOk, lane, geo.epoch);
+        break;
+    }
+    // piece 0: its start is exact; accept the pieces in order while each boundary check passed
+    if (split_commit(sflags, cmpOk, geo.epoch)) break;
+    if (lane == 0) {  // otherwise re-decode the whole chunk (pass 1) after stopping the pieces' writes
+        __hip_atomic_store(sflags + 12, geo.epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (geo.stats) atomicAdd(geo.stats, 1u);
+    }
+    }  // pass
     if constexpr (!(ABL & 256)) {
         if (fb && lane == 0) atomicAdd(fb, 0ull - ((1ull << 32) + fadded));
     }

@@ -44,6 +44,13 @@ struct Geom {
     uint32_t nchunks;
     unsigned long long* fair;  // per-SIMD progress board (kFairSlots words, zero at rest) or null
     float scale;               // LLR input (channel ids 8 + base): SoftDecisionPacker scale, else unused
+    // split launch (vd_kernel_tg.h "split chunks"): chunks >= nwhole are decoded as kWaves pieces, one
+    // workgroup each; 0 = every chunk whole
+    uint32_t nwhole = 0;
+    uint32_t epoch = 0;          // launch id carried by the split flags
+    float* spec = nullptr;       // [chunk - nwhole][kWaves][64] published metric vectors
+    uint32_t* flags = nullptr;   // [chunk - nwhole][16] split flags
+    uint32_t* stats = nullptr;   // count of split chunks re-decoded whole (or null)
 };
 // progress board: one 64-bit word per SIMD slot, (waves << 32) + blocks started; indexed by
 // (XCC, SE, SH, CU, SIMD) from the hardware wave id.  Only issue priority depends on it.

@@ -42,7 +42,7 @@ EXPORTS = ["vd_options_valid", "vd_input_size", "vd_message_len", "vd_output_siz
            "vd_create", "vd_destroy", "vd_run", "vd_run_device", "vd_run_batches", "vd_synth_device",
            "vd_simulate_host", "vd_count_errors", "vd_last_error", "vd_device_count", "vd_kernel_name",
            "vd_pack_device", "vd_run_device_llr", "vd_run_llr", "vd_host_alloc", "vd_host_free",
-           "vd_run_stream", "vd_channel_device", "vd_simulate_device", "vd_mt_state_after"]
+           "vd_run_stream", "vd_channel_device", "vd_simulate_device", "vd_mt_state_after", "vd_split_redecodes"]
 
 
 class VitdecError(RuntimeError):
@@ -76,6 +76,7 @@ def lib():
     L.vd_channel_device.argtypes = [sz, f, ctypes.c_uint32, ctypes.c_uint32, vp, vp, vp]
     L.vd_simulate_device.argtypes = [i, sz, f, ctypes.c_uint32, ctypes.c_uint32, vp, vp, vp]
     L.vd_mt_state_after.argtypes = [ctypes.c_uint32, ctypes.c_uint64, vp]
+    L.vd_split_redecodes.argtypes = [i, ctypes.POINTER(ctypes.c_uint64)]
     L.vd_count_errors.argtypes = [i, vp, sz, vp, sz]
     L.vd_count_errors.restype = ctypes.c_longlong
     L.vd_last_error.restype = ctypes.c_char_p
@@ -285,6 +286,13 @@ def simulate_device(options, n_bits, snr, bit_seed, noise_seed, bits_ptr, packed
     _check(lib().vd_simulate_device(options, n_bits, snr, bit_seed, noise_seed,
                                     ctypes.c_void_p(bits_ptr) if bits_ptr else None, ctypes.c_void_p(packed_ptr),
                                     ctypes.c_void_p(stream)))
+
+
+def split_redecodes(device=0):
+    """split chunks re-decoded whole on a device so far (a speculative piece start did not converge)"""
+    v = ctypes.c_uint64(0)
+    _check(lib().vd_split_redecodes(device, ctypes.byref(v)))
+    return v.value
 
 
 def mt_state_after(seed, n):

@@ -145,6 +145,10 @@ int vd_mt_state_after(uint32_t seed, uint64_t n, uint32_t* state624);
 long long vd_count_errors(int options, const uint8_t* bits, size_t N, const void* decoded, size_t decodedBytes);
 
 /* ---- runtime info ---- */
+/* split launches (DESIGN.md §4 "load balance"): how many split chunks were re-decoded whole on a device
+ * because a speculative piece start did not converge (all launches so far; decoded words are exact
+ * either way).  Set VD_NO_SPLIT=1 in the environment to disable splitting. */
+int vd_split_redecodes(int device, uint64_t* count);
 const char* vd_last_error(void);
 int vd_device_count(void);
 /* last decode kernel's name and grid, for profilers (static strings) */

