@@ -76,6 +76,13 @@ __device__ __forceinline__ int tg_pos(int l)
     const int p2 = (l >> 2) & 1;
     return (l & ~7) | (p2 << 2) | ((((l >> 1) & 1) ^ p2) << 1) | ((l & 1) ^ p2);
 }
+// alternative map (ABL 131072, timing study): l = p0*1 ^ p1*2 ^ p4*7 ^ p3*8 ^ p2*16 ^ p5*32
+__device__ __forceinline__ int tg_pos_b(int l)
+{
+    const int p4 = (l >> 2) & 1;
+    return ((l & 1) ^ p4) | ((((l >> 1) & 1) ^ p4) << 1) | (((l >> 4) & 1) << 2) | (((l >> 3) & 1) << 3) | (p4 << 4) |
+           (((l >> 5) & 1) << 5);
+}
 // reference label (0..3) of position p's own predecessor branch at stage phase k, and its parity helper
 __host__ __device__ constexpr int tg_par7(int v) { return (v & 1) ^ ((v >> 1) & 1) ^ ((v >> 2) & 1) ^ ((v >> 3) & 1) ^ ((v >> 4) & 1) ^ ((v >> 5) & 1) ^ ((v >> 6) & 1); }
 __host__ __device__ constexpr int tg_label(int p, int k)
@@ -424,7 +431,8 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(7))
     __shared__ __attribute__((aligned(256))) uint32_t ring_all[kWaves][(TBS + 1) * 64];  // bit 31-s = stage s
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int pos = tg_pos(lane);
+    constexpr bool MAPB = (ABL & 131072) != 0;
+    const int pos = MAPB ? tg_pos_b(lane) : tg_pos(lane);
     char* tabb = tab_all[wv];
     uint32_t* ring = ring_all[wv];
     // This wave's work: chunk blockIdx.x * kWaves + wv, or, in a split launch (Geom::nwhole), piece wv of
@@ -531,23 +539,26 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(7))
             // ABL (tools only): 2 = no table reads, 128 = every stage a DPP stage, 4 = no field read-out
             constexpr bool ODD = (r / 6) % 2 == 1;
             constexpr int RP = TT::pairrow(K) ? r : (ODD ? r - 6 : r);  // where this stage's pair was read
-            // Q=4 (lane xor 16) fetches the partner's metric through the LDS crossbar (ds_swizzle), Q=5
-            // (xor 32) swaps candidates with v_permlane32_swap: a VALU lane swap costs two issue slots, the
-            // swizzle none, and doing both through the LDS queues them behind each other and the table
-            // reads (tools/vd_swapab).  ABL (tools only): 16384 = Q=4 by v_permlane16_swap too,
-            // 8192 = Q=5 by ds_bpermute.
-            constexpr bool LSW = (Q == 5 && (ABL & 8192)) || (Q == 4 && !(ABL & 16384));
-            if constexpr (Q <= 3 || (ABL & 128)) {
+            // The position bit on lane xor 16 (Q=4; Q=2 with the ABL 131072 map) fetches the partner's
+            // metric through the LDS crossbar (ds_swizzle), Q=5 (xor 32) swaps candidates with
+            // v_permlane32_swap: a VALU lane swap costs two issue slots, the swizzle none, and doing both
+            // through the LDS queues them behind each other and the table reads (tools/vd_swapab).
+            // ABL (tools only): 16384 = xor 16 by v_permlane16_swap too, 8192 = Q=5 by ds_bpermute.
+            constexpr int X16 = MAPB ? 2 : 4;
+            constexpr bool IS16 = Q == X16, IS32 = Q == 5;
+            constexpr int DCTRL = MAPB && Q == 4 ? 2 : (Q <= 3 ? Q : 3);  // lane xor 1, 2, 7, 8 -> DPP control
+            constexpr bool LSW = (IS32 && (ABL & 8192)) || (IS16 && !(ABL & 16384));
+            if constexpr ((!IS16 && !IS32) || (ABL & 128)) {
                 const float m = (ABL & 2) ? (float)aK[K] : (ODD ? vp[RP].y : vp[RP].x);
-                tg_stage_dpp<(Q <= 3 ? Q : 3)>(V, m);
+                tg_stage_dpp<DCTRL>(V, m);
             } else if constexpr (LSW) {
-                const float pv = Q == 4 ? __builtin_bit_cast(float, __builtin_amdgcn_ds_swizzle(__builtin_bit_cast(int, V), 0x401F))
-                                        : tg_partner(V, pa5);
+                const float pv = IS16 ? __builtin_bit_cast(float, __builtin_amdgcn_ds_swizzle(__builtin_bit_cast(int, V), 0x401F))
+                                      : tg_partner(V, pa5);
                 const f2v e = (ABL & 2) ? (f2v){(float)aK[K], 1.0f} : vp[RP];
                 tg_stage_lds<TT::pairrow(K) ? 2 : (ODD ? 1 : 0)>(V, e, pv, upper5);
             } else {
                 const f2v e = (ABL & 2) ? (f2v){(float)aK[K], 1.0f} : vp[RP];
-                tg_stage_swap<Q, TT::pairrow(K) ? 2 : (ODD ? 1 : 0), (ABL >> 10) & 7>(V, e, sxp[K == 0 ? 0 : 1]);
+                tg_stage_swap<IS16 ? 4 : 5, TT::pairrow(K) ? 2 : (ODD ? 1 : 0), (ABL >> 10) & 7>(V, e, sxp[K == 0 ? 0 : 1]);
             }
             if constexpr (r + TGD < 96) issue(std::integral_constant<int, r + TGD>{});
             if constexpr (i % J == J - 1 && !(ABL & 4)) {

@@ -27,9 +27,10 @@ int main(int argc, char** argv)
     g.scale = 1.0f;
     CK(hipMalloc(&g.fair, vd::kFairSlots * 8));
     CK(hipMemset(g.fair, 0, vd::kFairSlots * 8));
-    std::vector<Var> v = {hb<0>("full (Q4 swizzle)"), hb<16384>("Q4 permlane16 (previous)"), hb<8192>("Q4 swizzle + Q5 bpermute"),
-                          hb<128>("all-dpp"), hb<16384 | 1024>("swaps without lane movement"),
-                          hb<1 | 2 | 4 | 8 | 16>("ACS only"), hb<1 | 2 | 4 | 8 | 16 | 128>("ACS only all-dpp")};
+    std::vector<Var> v = {hb<0>("full (xor16 swizzle q4)"), hb<131072>("map B: swizzle q2, permlane q5"),
+                          hb<131072 | 8192>("map B: swizzle q2, bpermute q5"), hb<8192>("map A: swizzle q4, bpermute q5"),
+                          hb<128>("all-dpp"), hb<1 | 2 | 4 | 8 | 16>("ACS only"), hb<1 | 2 | 4 | 8 | 16 | 131072 | 8192>("ACS only, map B both LDS"),
+                          hb<1 | 2 | 4 | 8 | 16 | 128>("ACS only all-dpp")};
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
     const int rounds = argc > 1 ? atoi(argv[1]) : 10;
