@@ -317,8 +317,8 @@ def main():
         # VALU issue view of the same kernel (the bound that actually binds)
         stages = stages_per_launch(db["opt"], db["input_num"])
         valu = None
-        if "valu_insts_per_wave" in pmc:
-            insts = pmc["valu_insts_per_wave"] * vitdec.lib().vd_num_chunks()
+        if "counters_mean_per_dispatch" in pmc and "SQ_INSTS_VALU" in pmc["counters_mean_per_dispatch"]:
+            insts = pmc["counters_mean_per_dispatch"]["SQ_INSTS_VALU"]  # all waves of the launch (split pieces too)
             valu = {"insts_per_launch": round(insts), "insts_per_wave_stage": round(insts / stages, 3),
                     "wave_stages_per_launch": stages,
                     "issue_cycles_per_inst_per_simd": round(kms[di] * 1e-3 * CLOCK_HZ * N_SIMD / insts, 3),
