@@ -63,10 +63,23 @@ def cpu_baseline(batches):
         gpu = b["out"].cpu().numpy().view(out.dtype)
         match = match and bool(np.array_equal(out, gpu))
     names = " + ".join(b["name"] for b in batches)
+    # (ii) of SURVEY 8d: the same restatement over the independent chunks on every host thread this
+    # process may use (the GPU box gives a job a 16-CPU share; os.cpu_count() shows the whole machine)
+    nt = max(1, min(16, len(os.sched_getaffinity(0))))
+    dt_mt = 0.0
+    for b in batches:
+        packed = b["inp"].cpu().numpy().view(np.float32 if (b["opt"] & 0xF) == vitdec.FP32 else np.int32)
+        t0 = time.perf_counter()
+        out, _ = vo.decode(b["opt"], packed, input_num=b["input_num"], nthreads=nt)
+        dt_mt += time.perf_counter() - t0
+        gpu = b["out"].cpu().numpy().view(out.dtype)
+        match = match and bool(np.array_equal(out, gpu))
+    all_cores = {"value": round(bits / dt_mt / 1e9, 6), "unit": "Gb/s", "cores": nt,
+                 "sample": f"the same step on {nt} host threads (chunks split across threads) in {dt_mt:.2f} s"}
     return {"value": round(bits / dt / 1e9, 6), "unit": "Gb/s", "cores": 1, "kind": "port",
             "sample": f"one full bench step ({names}, 2 x 32M-bit batches, 6400-chunk partition) decoded by "
                       f"oracle/vd_oracle.c on 1 host thread in {dt:.1f} s; output identical to the GPU's: {match}",
-            "matches_gpu": match}
+            "matches_gpu": match, "all_cores": all_cores}
 
 
 def load_pmc():
@@ -121,6 +134,71 @@ def gather_checksums(sums, dev, world):
     gathered = [torch.empty_like(cs) for _ in range(world)]
     torch.distributed.all_gather(gathered, cs)
     return [[int(v) for v in g.cpu()] for g in gathered]
+
+
+def gather_outputs(outs, dev, world, rank):
+    """The north_star's final gather: every rank's decoded words (uint8 tensors, equal sizes) to rank 0
+    over RCCL (gloo on CPU in tests/test_dist.py).  Outside the timed region.  Returns (ms, per-rank
+    XOR checksums of what rank 0 received) on rank 0, (ms, None) elsewhere."""
+    flat = torch.cat([o.view(-1) for o in outs])
+    bufs = [torch.empty_like(flat) for _ in range(world)] if rank == 0 else None
+    torch.distributed.barrier()
+    if flat.is_cuda:
+        torch.cuda.synchronize()
+    t = time.perf_counter()
+    torch.distributed.gather(flat, bufs, dst=0)
+    if flat.is_cuda:
+        torch.cuda.synchronize()
+    ms = (time.perf_counter() - t) * 1e3
+    if rank != 0:
+        return ms, None
+    sums = []
+    for b in bufs:
+        parts, off = [], 0
+        for o in outs:
+            n = o.numel()
+            parts.append(int(np.bitwise_xor.reduce(b[off:off + n].cpu().numpy().view(np.uint32))))
+            off += n
+        sums.append(parts)
+    return ms, sums
+
+
+OTHER_CONFIGS = [
+    ("fp32_f16", vitdec.FP32 | vitdec.M_FP16 | vitdec.O_B32),   # BASELINE configs[4]
+    ("soft4_b16", vitdec.SOFT4 | vitdec.M_B16 | vitdec.O_B32),
+    ("soft16_b32", vitdec.SOFT16 | vitdec.M_B32 | vitdec.O_B32),
+    ("hard_b32_ob16", vitdec.HARD | vitdec.M_B32 | vitdec.O_B16),
+]
+
+
+def other_configs_side_measurement(dev, sptr, stream, reps=5):
+    """Kernel-only Gb/s of the other input formats / cores at 32M bits (BASELINE configs[4] = FP32 input
+    on the fp16 core, plus SOFT4, SOFT16 and 16-bit output words), inputs synthesised by the GPU channel
+    source at the bench SNR.  Outside the timed region; never `value`."""
+    res = {}
+    for i, (name, opt) in enumerate(OTHER_CONFIGS):
+        n = 2 * N_BITS
+        inp = torch.empty(vitdec.lib().vd_input_size(opt, n), dtype=torch.uint8, device=dev)
+        bits = torch.empty(N_BITS, dtype=torch.uint8, device=dev)
+        out = torch.empty(vitdec.lib().vd_output_size(opt, n), dtype=torch.uint8, device=dev)
+        vitdec.simulate_device(opt, N_BITS, SNR_DB, 101 + 2 * i, 102 + 2 * i, bits.data_ptr(), inp.data_ptr(), sptr)
+        dec = vitdec.ViterbiCUDA(opt, 0, dev)
+        run = lambda: dec.run_device(inp.data_ptr(), out.data_ptr(), n, sptr)
+        run()
+        e = [torch.cuda.Event(enable_timing=True) for _ in range(2 * reps)]
+        for r in range(reps):
+            e[2 * r].record(stream)
+            run()
+            e[2 * r + 1].record(stream)
+        torch.cuda.synchronize()
+        ms = float(np.median([e[2 * r].elapsed_time(e[2 * r + 1]) for r in range(reps)]))
+        msg = vitdec.lib().vd_message_len(opt, n)
+        dt = np.uint16 if (opt & 0xF00) == vitdec.O_B16 else np.uint32
+        ber = vitdec.count_errors(opt, bits.cpu().numpy(), out.cpu().numpy().view(dt)) / msg
+        res[name] = {"kernel": vitdec.kernel_name(opt), "kernel_ms": round(ms, 4),
+                     "gbps": round(msg / (ms * 1e-3) / 1e9, 2), "ber": ber}
+        dec.close()
+    return res
 
 
 def llr_side_measurement(dev, sptr, stream, reps=5):
@@ -225,6 +303,7 @@ def main():
     ap.add_argument("--no-llr", action="store_true", help="skip the float-input (packer fused) side measurement")
     ap.add_argument("--no-pcie", action="store_true", help="skip the host-to-host pipelined side measurement")
     ap.add_argument("--no-channel", action="store_true", help="skip the channel-source side measurement")
+    ap.add_argument("--no-other", action="store_true", help="skip the other-formats side measurement")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -297,9 +376,18 @@ def main():
     llr = None if args.no_llr else llr_side_measurement(dev, sptr, stream)
     pcie = None if args.no_pcie else pcie_side_measurement(batches, dev)
     chan = None if (args.no_channel or rank != 0) else channel_side_measurement(dev, sptr)
+    other = None if (args.no_other or rank != 0) else other_configs_side_measurement(dev, sptr, stream)
+    final_gather = None
     if world > 1:
         elapsed = max_over_ranks(elapsed, dev)
         gathered = gather_checksums(sums, dev, world)
+        gms, gsums = gather_outputs([b["out"] for b in batches], dev, world, rank)
+        if rank == 0:
+            nbytes = sum(b["out"].numel() for b in batches)
+            final_gather = {"what": "every rank's decoded words to rank 0 (torch.distributed.gather over RCCL)",
+                            "bytes_per_rank": nbytes, "ms": round(gms, 3),
+                            "GBps_into_rank0": round(nbytes * (world - 1) / (gms * 1e-3) / 1e9, 2),
+                            "checksums_match": gsums == gathered}
     else:
         gathered = [sums]
 
@@ -370,6 +458,10 @@ def main():
             result["config"]["pcie_inclusive"] = pcie
         if chan is not None:
             result["config"]["channel_source"] = chan
+        if other is not None:
+            result["config"]["other_configs"] = other
+        if final_gather is not None:
+            result["config"]["final_gather"] = final_gather
         if not args.no_cpu_baseline and world == 1:
             result["cpu_baseline"] = cpu_baseline(batches)
         print(json.dumps(result), flush=True)

@@ -24,6 +24,15 @@ def _free_port():
     return p
 
 
+def _outs(rank):
+    return [torch.arange(16, dtype=torch.uint8) * 3 + 40 * rank, torch.arange(8, dtype=torch.uint8) + 7 * rank + 1]
+
+
+def _xor_words(t):
+    import numpy as np
+    return int(np.bitwise_xor.reduce(t.numpy().view(np.uint32)))
+
+
 def _worker(rank, world, port, q):
     sys.path.insert(0, ROOT)
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
@@ -34,7 +43,10 @@ def _worker(rank, world, port, q):
     sums = [0xDEAD0000 + rank, 0xBEEF0000 + rank]  # uint32 checksums, as bench computes them
     g = bench.gather_checksums(sums, "cpu", world)
     seeds = [bench.rank_seed(rank, wi) for wi in range(2)]
-    q.put((rank, m, g, seeds))
+    # the final gather of decoded words (uint8 buffers, as the decode writes them) to rank 0
+    outs = _outs(rank)
+    _, gs = bench.gather_outputs(outs, "cpu", world, rank)
+    q.put((rank, m, g, seeds, gs))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -51,10 +63,15 @@ def test_two_rank_gloo_sharding():
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    for rank, m, g, seeds in res:
+    for rank, m, g, seeds, gs in res:
         assert m == 2.0  # max over ranks
         assert g == [[0xDEAD0000, 0xBEEF0000], [0xDEAD0001, 0xBEEF0001]]
-    all_seeds = [s for _, _, _, seeds in res for s in seeds]
+        if rank == 0:  # rank 0 received every rank's words intact
+            want = [[_xor_words(o) for o in _outs(r)] for r in range(world)]
+            assert gs == want and want[0] != want[1]
+        else:
+            assert gs is None
+    all_seeds = [s for _, _, _, seeds, _ in res for s in seeds]
     assert len(set(all_seeds)) == len(all_seeds)  # every rank decodes independent batches
 
 

@@ -142,3 +142,29 @@ def test_parity_full_32m(gpu, vo, opt):
     out = gpu_decode(gpu, opt, packed)
     np.testing.assert_array_equal(out, ref)
     assert gpu.count_errors(opt, bits, out) == vo.ben(opt, bits, ref)
+
+
+@pytest.mark.gpu
+@pytest.mark.slow
+def test_parity_full_32m_fp32_fp16(gpu, vo):
+    # BASELINE configs[4]: 32M bits, FP32 soft input on the fp16 path-metric core, every word (tolerance 0)
+    opt = FP32 | M_FP16
+    bits, packed = vo.simulate(opt, 32_000_000, 1.2, 3, 4)
+    ref, ok = vo.decode(opt, packed, nthreads=16)
+    assert ok
+    out = gpu_decode(gpu, opt, packed)
+    np.testing.assert_array_equal(out, ref)
+
+
+@pytest.mark.gpu
+@pytest.mark.slow
+def test_parity_256m_one_stream(gpu, vo):
+    # BASELINE configs[3]'s 256M bits as ONE stream on one GPU (base = 1249 words per chunk):
+    # long chunks, 40 traceback batches each; every word against the oracle, and the BEN equal
+    opt = SOFT8 | M_B16
+    bits, packed = vo.simulate(opt, 256_000_000, 1.3, 9, 10)
+    ref, ok = vo.decode(opt, packed, nthreads=16)
+    assert ok and ref.size == 255_999_936 // 32
+    out = gpu_decode(gpu, opt, packed)
+    np.testing.assert_array_equal(out, ref)
+    assert gpu.count_errors(opt, bits, out) == vo.ben(opt, bits, ref)
