@@ -113,6 +113,38 @@ __device__ __forceinline__ void tg_stage_dpp(float& V, float m)
     else VD_TG_DPP("row_ror:8");
 #undef VD_TG_DPP
 }
+// DPP stage, two ops: the butterfly partner has the same branch label in every phase (and, outside
+// M_B32's phase-0 swap rows, the same tag), so its V_exch - m is what this lane would compute from its own
+// V.  One v_pk_fma_f32 forms [a, b] = [V + m, V - m] in every lane, and the max takes b from the partner
+// through the DPP operand: V' = max(a, dpp(b)).  v_add/v_sub/v_fma issue in half the cycles of a DPP op
+// or a v_max (tools/vd_ubench11), so this beats add + sub_dpp + max.  b is read by DPP 2 slots after its
+// write (s_nop 1).  SEL as tg_stage_swap (0 = even period, 1 = odd period of the entry pair e).
+template <int Q, int SEL, bool PK>
+__device__ __forceinline__ void tg_stage_dpp2(float& V, f2v e, f2v s)
+{
+    const float m = SEL == 0 ? e.x : e.y;
+#define VD_TG_DPP2(CTRL)                                                                                     \
+    if constexpr (PK) {                                                                                      \
+        if constexpr (SEL == 0)                                                                              \
+            asm("v_pk_fma_f32 v[62:63], %1, %2, v[60:61] op_sel:[0,0,0] op_sel_hi:[0,1,0]\n\ts_nop 1\n\t"     \
+                "v_max_f32_dpp %0, v63, v62 " CTRL " row_mask:0xf bank_mask:0xf"                               \
+                : "+{v60}"(V) : "v"(e), "v"(s) : "v62", "v63");                                              \
+        else                                                                                                 \
+            asm("v_pk_fma_f32 v[62:63], %1, %2, v[60:61] op_sel:[1,0,0] op_sel_hi:[1,1,0]\n\ts_nop 1\n\t"     \
+                "v_max_f32_dpp %0, v63, v62 " CTRL " row_mask:0xf bank_mask:0xf"                               \
+                : "+{v60}"(V) : "v"(e), "v"(s) : "v62", "v63");                                              \
+    } else {                                                                                                 \
+        float a, b;                                                                                          \
+        asm("v_sub_f32 %2, %0, %3\n\tv_add_f32 %1, %0, %3\n\ts_nop 0\n\t"                                  \
+            "v_max_f32_dpp %0, %2, %1 " CTRL " row_mask:0xf bank_mask:0xf"                                     \
+            : "+{v60}"(V), "=&v"(a), "=&v"(b) : "v"(m));                                                    \
+    }
+    if constexpr (Q == 0) { VD_TG_DPP2("quad_perm:[1,0,3,2]") }
+    else if constexpr (Q == 1) { VD_TG_DPP2("quad_perm:[2,3,0,1]") }
+    else if constexpr (Q == 2) { VD_TG_DPP2("row_half_mirror") }
+    else { VD_TG_DPP2("row_ror:8") }
+#undef VD_TG_DPP2
+}
 // swap stage, exchange lane xor 16 (Q=4) or 32 (Q=5): [a, b] = [m, m'] * [sx, -sx] + [V, V] in one
 // v_pk_fma_f32, swap halves across lanes, max.  The butterfly partner has the same label in both swap
 // phases, so m' = m except in M_B32's phase-0 rows (m, m' = the two tag signs).  SEL picks the halves of
@@ -458,6 +490,7 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(7))
     });
     const int pa5 = 4 * (lane ^ 32);  // ds_bpermute address of the xor-32 partner (tools variant)
     const bool upper5 = (pos >> 5) & 1;
+    const f2v spm = (f2v){1.0f, -1.0f};  // [a, b] = [V + m, V - m] of the two-op DPP stage
     f2v sxp[2];
     sfor<2>([&](auto W) {
         constexpr int w = decltype(W)::value;  // 0: K=0 (Q=5), 1: K=5 (Q=4)
@@ -548,7 +581,11 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(7))
             constexpr bool IS16 = Q == X16, IS32 = Q == 5;
             constexpr int DCTRL = MAPB && Q == 4 ? 2 : (Q <= 3 ? Q : 3);  // lane xor 1, 2, 7, 8 -> DPP control
             constexpr bool LSW = (IS32 && (ABL & 8192)) || (IS16 && !(ABL & 16384));
-            if constexpr ((!IS16 && !IS32) || (ABL & 128)) {
+            if constexpr (((!IS16 && !IS32) || (ABL & 128)) && (ABL & (262144 | 524288)) && !TT::pairrow(K)) {
+                // ABL (tools only): 262144 = sub, add, max_dpp; 524288 = pk_fma, max_dpp
+                const f2v e = (ABL & 2) ? (f2v){(float)aK[K], 1.0f} : vp[RP];
+                tg_stage_dpp2<DCTRL, ODD ? 1 : 0, (ABL & 524288) != 0>(V, e, spm);
+            } else if constexpr ((!IS16 && !IS32) || (ABL & 128)) {
                 const float m = (ABL & 2) ? (float)aK[K] : (ODD ? vp[RP].y : vp[RP].x);
                 tg_stage_dpp<DCTRL>(V, m);
             } else if constexpr (LSW) {

@@ -45,6 +45,8 @@ int main(int argc, char** argv)
     tgb<2>(v, "tg hard/b32 -tabreads"); tgb<4>(v, "tg hard/b32 -readout"); tgb<8>(v, "tg hard/b32 -tabbuild"); tgb<128>(v, "tg hard/b32 all-dpp"); tgb<512>(v, "tg hard/b32 -tabwrites"); tgs<512>(v, "tg soft8/b16 -tabwrites"); tgs<8>(v, "tg soft8/b16 -tabbuild");
     tgb<2 | 4 | 8 | 16 | 1>(v, "tg hard/b32 ACS only"); tgb<2 | 4 | 8 | 16 | 1 | 128>(v, "tg hard/b32 ACS only all-dpp");
     tgs<0>(v, "tg soft8/b16 full"); tgs<1>(v, "tg soft8/b16 -traceback"); tgs<2>(v, "tg soft8/b16 -tabreads"); tgs<4>(v, "tg soft8/b16 -readout"); tgf<0>(v, "tg fp32/f16 full");
+    tgb<262144>(v, "tg hard/b32 sub+add+maxdpp"); tgs<262144>(v, "tg soft8/b16 sub+add+maxdpp");
+    tgb<524288>(v, "tg hard/b32 pkfma+maxdpp"); tgs<524288>(v, "tg soft8/b16 pkfma+maxdpp");
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
     const int rounds = argc > 1 ? atoi(argv[1]) : 10;
