@@ -76,10 +76,23 @@ def cpu_baseline(batches):
         match = match and bool(np.array_equal(out, gpu))
     all_cores = {"value": round(bits / dt_mt / 1e9, 6), "unit": "Gb/s", "cores": nt,
                  "sample": f"the same step on {nt} host threads (chunks split across threads) in {dt_mt:.2f} s"}
-    return {"value": round(bits / dt / 1e9, 6), "unit": "Gb/s", "cores": 1, "kind": "port",
+    return {"value": round(bits / dt / 1e9, 6), "unit": "Gb/s", "cores": 1, "kind": "port", "cpu_model": cpu_model(),
             "sample": f"one full bench step ({names}, 2 x 32M-bit batches, 6400-chunk partition) decoded by "
                       f"oracle/vd_oracle.c on 1 host thread in {dt:.1f} s; output identical to the GPU's: {match}",
             "matches_gpu": match, "all_cores": all_cores}
+
+
+def cpu_model():
+    """Host CPU model name (report the CPU next to the core count)."""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    import platform
+    return platform.processor() or "unknown"
 
 
 def load_pmc():
@@ -140,9 +153,19 @@ def gather_outputs(outs, dev, world, rank):
     """The north_star's final gather: every rank's decoded words (uint8 tensors, equal sizes) collected
     over RCCL (ncclAllGather, the collective bench already uses for its checksums; gloo on CPU in
     tests/test_dist.py).  Outside the timed region.  Returns (ms, per-rank XOR checksums of what rank 0
-    received) on rank 0, (ms, None) elsewhere."""
-    flat = torch.cat([o.view(-1) for o in outs])
-    bufs = [torch.empty_like(flat) for _ in range(world)]
+    received, None) on rank 0, (ms, None, None) elsewhere, or (None, None, error) on every rank when any
+    rank could not allocate its receive buffers: the ranks agree on that (all_reduce of an ok flag)
+    before anyone enters the collective, so no rank is left waiting in it."""
+    err = None
+    try:
+        flat = torch.cat([o.view(-1) for o in outs])
+        bufs = [torch.empty_like(flat) for _ in range(world)]
+    except Exception as e:  # e.g. torch.OutOfMemoryError on this rank only
+        err = str(e)[:200]
+    ok = torch.tensor([0 if err else 1], dtype=torch.int32, device=dev)
+    torch.distributed.all_reduce(ok, op=torch.distributed.ReduceOp.MIN)
+    if int(ok.item()) == 0:
+        return None, None, err or "a peer rank could not allocate its all_gather buffers"
     torch.distributed.barrier()
     if flat.is_cuda:
         torch.cuda.synchronize()
@@ -152,7 +175,7 @@ def gather_outputs(outs, dev, world, rank):
         torch.cuda.synchronize()
     ms = (time.perf_counter() - t) * 1e3
     if rank != 0:
-        return ms, None
+        return ms, None, None
     sums = []
     for b in bufs:
         parts, off = [], 0
@@ -161,7 +184,7 @@ def gather_outputs(outs, dev, world, rank):
             parts.append(int(np.bitwise_xor.reduce(b[off:off + n].cpu().numpy().view(np.uint32))))
             off += n
         sums.append(parts)
-    return ms, sums
+    return ms, sums, None
 
 
 OTHER_CONFIGS = [
@@ -295,6 +318,30 @@ def pcie_side_measurement(batches, dev, nb=6):
     return res
 
 
+def launch_ranks(nproc, argv):
+    """`bench.py --gpus N` (N > 1) without a torch.distributed launcher: start N ranks with
+    torch.distributed.run as a CHILD process (this process has not touched the GPU and never will), pass
+    its output through, and return its exit code.  Each rank re-enters main() with WORLD_SIZE set."""
+    import socket
+    import subprocess
+    with socket.socket() as s:  # a free rendezvous port on the loopback interface
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__), *argv]
+    return subprocess.call(cmd)
+
+
+def ranks_check(world, rank):
+    """--ranks-check (tests): the rank layout `--gpus N` produces, over gloo, no GPU touched."""
+    torch.distributed.init_process_group("gloo")
+    got = [None] * world
+    torch.distributed.all_gather_object(got, {"rank": rank, "local_rank": int(os.environ.get("LOCAL_RANK", "0"))})
+    if rank == 0:
+        print(json.dumps({"n_gpus": world, "ranks": got}), flush=True)
+    torch.distributed.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -305,11 +352,26 @@ def main():
     ap.add_argument("--no-pcie", action="store_true", help="skip the host-to-host pipelined side measurement")
     ap.add_argument("--no-channel", action="store_true", help="skip the channel-source side measurement")
     ap.add_argument("--no-other", action="store_true", help="skip the other-formats side measurement")
+    ap.add_argument("--ranks-check", action="store_true", help=argparse.SUPPRESS)  # tests: rank layout only
     args = ap.parse_args()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.gpus < 1:
+        sys.exit(f"bench.py: --gpus must be >= 1 (got {args.gpus})")
+    if "WORLD_SIZE" not in os.environ:
+        if args.gpus > 1:  # one process per GPU: start the ranks as children, before any GPU call here
+            sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+        world = 1
+    else:
+        world = int(os.environ["WORLD_SIZE"])
+        if world != args.gpus:
+            sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; launch one rank per GPU "
+                     f"(torch.distributed.run --nproc-per-node {args.gpus}) or drop the launcher")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.ranks_check:
+        return ranks_check(world, rank)
+    if not args.ranks_check and torch.cuda.device_count() < world:
+        sys.exit(f"bench.py: {world} ranks but only {torch.cuda.device_count()} visible GPU(s)")
     if world > 1:
         torch.cuda.set_device(local)
         torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local))
@@ -374,24 +436,24 @@ def main():
         out_h = b["out"].cpu().numpy().view(dt)
         bers.append(vitdec.count_errors(b["opt"], bits_h, out_h) / b["msg"])
         sums.append(int(np.bitwise_xor.reduce(out_h.view(np.uint32))))
-    llr = None if args.no_llr else llr_side_measurement(dev, sptr, stream)
-    pcie = None if args.no_pcie else pcie_side_measurement(batches, dev)
+    llr = None if (args.no_llr or rank != 0) else llr_side_measurement(dev, sptr, stream)
+    pcie = None if (args.no_pcie or rank != 0) else pcie_side_measurement(batches, dev)
     chan = None if (args.no_channel or rank != 0) else channel_side_measurement(dev, sptr)
     other = None if (args.no_other or rank != 0) else other_configs_side_measurement(dev, sptr, stream)
     final_gather = None
     if world > 1:
         elapsed = max_over_ranks(elapsed, dev)
         gathered = gather_checksums(sums, dev, world)
-        try:
-            gms, gsums = gather_outputs([b["out"] for b in batches], dev, world, rank)
-            if rank == 0:
+        gms, gsums, err = gather_outputs([b["out"] for b in batches], dev, world, rank)
+        if rank == 0:
+            if err is not None:  # a side measurement: report it, keep the bench line
+                final_gather = {"error": err}
+            else:
                 nbytes = sum(b["out"].numel() for b in batches)
                 final_gather = {"what": "every rank's decoded words collected over RCCL (all_gather)",
                                 "bytes_per_rank": nbytes, "ms": round(gms, 3),
                                 "GBps_into_each_rank": round(nbytes * (world - 1) / (gms * 1e-3) / 1e9, 2),
                                 "checksums_match": gsums == gathered}
-        except RuntimeError as e:  # a side measurement: report it, keep the bench line
-            final_gather = {"error": str(e)[:200]}
     else:
         gathered = [sums]
 
@@ -426,7 +488,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "int32+int16x2",
+            "dtype": "fp32 exact-integer (int32/int16 tie semantics)",
             "data": f"synthetic: the reference harness chain generated on the GPU bit-exactly (std::mt19937 "
                     f"bits, K=7 (0171,0133) encoder, BPSK + normal_distribution<float> AWGN at {SNR_DB} dB, "
                     f"quantiser scale 40000), seeds (1+2i, 2+2i) for batch i = 2 rank + workload",

@@ -22,7 +22,6 @@
 #include "vd_kernels.h"
 #include "vd_kernel_tg.h"
 #include "vd_pack.h"
-#include "vd_synth.h"
 #include "vd_mt.h"
 #include "vd_mtjump.h"
 
@@ -188,6 +187,7 @@ static void* mapped_host(const void* p)
     return a.type == hipMemoryTypeHost ? a.devicePointer : nullptr;
 }
 
+struct DeviceState;
 struct vd_decoder {
     int options = 0;
     int device = 0;
@@ -202,6 +202,8 @@ struct vd_decoder {
     void* out2_d = nullptr;
     size_t cap2_in = 0, cap2_out = 0;
     hipStream_t s_in = nullptr, s_out = nullptr;
+    DeviceState* ds = nullptr;  // the device's board / split state (looked up once, vd_create)
+    bool split = true;          // split launches allowed (VD_NO_SPLIT=1 at vd_create: no)
 };
 
 static int ensure_capacity(vd_decoder* d, size_t inBytes, size_t outBytes)
@@ -223,89 +225,68 @@ static int ensure_capacity(vd_decoder* d, size_t inBytes, size_t outBytes)
     return VD_OK;
 }
 
-// Per-device progress board of the decode kernels' fairness controller (vd_kernels.h, Geom::fair).
-// Allocated and zeroed once per device, shared by every decoder and stream on it: the kernels
-// leave it at zero, and concurrent launches sharing it only perturb issue priorities.
-static unsigned long long* fair_board(int device)
-{
-    static std::mutex mu;
-    static std::vector<unsigned long long*> boards;
-    std::lock_guard<std::mutex> lk(mu);
-    if ((int)boards.size() <= device) boards.resize(device + 1, nullptr);
-    if (!boards[device]) {
-        void* p = nullptr;
-        if (hipMalloc(&p, vd::kFairSlots * sizeof(unsigned long long)) != hipSuccess) return nullptr;
-        if (hipMemset(p, 0, vd::kFairSlots * sizeof(unsigned long long)) != hipSuccess ||
-            hipDeviceSynchronize() != hipSuccess) {
-            (void)hipFree(p);
-            return nullptr;
-        }
-        boards[device] = (unsigned long long*)p;
-    }
-    return boards[device];
-}
-
-// Per-device bookkeeping of split launches (vd_kernel_tg.h "split chunks"): kSplitSlots slots, a launch
-// uses slot epoch % kSplitSlots, so up to that many split launches may be in flight on a device at once.
-constexpr int kSplitSlots = 16;
-struct SplitState {
+// Per-device state shared by every decoder and stream on a device, allocated once per device:
+//  * the progress board of the decode kernels' fairness controller (vd_kernels.h Fair, Geom::fair),
+//    every word kFairEmpty at rest (the kernels free their slots); concurrent launches sharing it only
+//    perturb issue priorities;
+//  * the boundary vectors of split launches (vd_kernel_tg.h "split chunks"): kSplitSlots slots, a launch
+//    takes the next one, so up to kSplitSlots split launches may run on a device at once (far more than
+//    the hardware queues a process gets);
+//  * the re-decode counter (vd_split_redecodes).
+// A decoder looks it up once (vd_create), not per launch.
+constexpr int kSplitSlots = 32;
+struct DeviceState {
+    uint32_t* board = nullptr;
     int nsimd = 0;
-    uint32_t maxSplit = 0;      // split chunks a slot holds
-    float* spec = nullptr;      // [slot][maxSplit][kWaves][64]
-    uint32_t* flags = nullptr;  // [slot][maxSplit][16]
-    uint32_t* stats = nullptr;  // re-decoded split chunks (all launches)
-    std::atomic<uint32_t> epoch{0};
+    uint32_t maxSplit = 0;  // split chunks a slot holds
+    float* spec = nullptr;  // [slot][maxSplit][kSplitVecs][64]
+    uint32_t* stats = nullptr;
+    std::atomic<uint32_t> next{0};
 };
-static SplitState* split_state(int device)
+static DeviceState* device_state(int device)
 {
     static std::mutex mu;
-    static std::vector<SplitState*> st;
+    static std::vector<DeviceState*> st;
     std::lock_guard<std::mutex> lk(mu);
     if ((int)st.size() <= device) st.resize(device + 1, nullptr);
     if (!st[device]) {
         int cus = 0;
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus <= 0)
             return nullptr;
-        SplitState* x = new SplitState;
+        DeviceState* x = new DeviceState;
         x->nsimd = 4 * cus;
         x->maxSplit = (uint32_t)(x->nsimd / vd::kWaves);
-        const size_t nspec = (size_t)kSplitSlots * x->maxSplit * vd::kWaves * 64, nflag = (size_t)kSplitSlots * x->maxSplit * 16;
-        if (hipMalloc(&x->spec, nspec * 4) != hipSuccess || hipMalloc(&x->flags, (nflag + 1) * 4) != hipSuccess ||
-            hipMemset(x->flags, 0, (nflag + 1) * 4) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
+        const size_t nspec = (size_t)kSplitSlots * x->maxSplit * vd::kSplitVecs * 64;
+        if (hipMalloc(&x->board, vd::kFairBoardWords * 4) != hipSuccess ||
+            hipMemset(x->board, 0xFF, vd::kFairBoardWords * 4) != hipSuccess ||
+            hipMalloc(&x->spec, nspec * 4) != hipSuccess || hipMalloc(&x->stats, 4) != hipSuccess ||
+            hipMemset(x->stats, 0, 4) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
             delete x;
             return nullptr;
         }
-        x->stats = x->flags + nflag;
         st[device] = x;
     }
     return st[device];
 }
 // split the launch when the chunks leave a remainder of exactly one piece wave per SIMD (6400 chunks
 // on 1024 SIMDs: 6 whole chunks per SIMD + 256 chunks in 4 pieces) and the chunks are long enough
-static void plan_split(vd::Geom& g, int options, int device)
+static void plan_split(vd::Geom& g, int options, DeviceState* x)
 {
     if (out_of(options) != 0 || ch_of(options) == vd::SOFT16) return;  // O_B32, tagged kernel only
-    if (const char* e = std::getenv("VD_NO_SPLIT"))
-        if (e[0] == '1') return;
-    SplitState* x = split_state(device);
-    if (!x) return;
     const uint32_t perSimd = g.nchunks / (uint32_t)x->nsimd, rem = g.nchunks % (uint32_t)x->nsimd;
     if (rem == 0 || rem * vd::kWaves != (uint32_t)x->nsimd || perSimd + 1 > 7) return;
     if (g.packNum / g.nchunks < (uint64_t)vd::kSplitMinWords) return;
-    uint32_t e = x->epoch.fetch_add(1) + 1;
-    if (e == 0) e = x->epoch.fetch_add(1) + 1;  // 0 marks "never set"
-    const uint32_t slot = e % kSplitSlots;
+    const uint32_t slot = x->next.fetch_add(1) % kSplitSlots;
     g.nwhole = g.nchunks - rem;
-    g.epoch = e;
-    g.spec = x->spec + (size_t)slot * x->maxSplit * vd::kWaves * 64;
-    g.flags = x->flags + (size_t)slot * x->maxSplit * 16;
+    g.spec = x->spec + (size_t)slot * x->maxSplit * vd::kSplitVecs * 64;
     g.stats = x->stats;
 }
 
 // llr: in_d holds inputNum float channel values, quantised in the kernel (scale = packer scale)
-static int launch_decode(int options, const void* in_d, void* out_d, size_t inputNum, hipStream_t s,
+static int launch_decode(const vd_decoder* d, const void* in_d, void* out_d, size_t inputNum, hipStream_t s,
                          bool llr = false, float scale = 1.0f)
 {
+    const int options = d->options;
     launch_fn f = llr ? pick_llr(options) : pick(options);
     if (!f) return fail(VD_ERR_OPTIONS, "invalid options");
     size_t msg = message_len(options, inputNum);
@@ -315,11 +296,8 @@ static int launch_decode(int options, const void* in_d, void* out_d, size_t inpu
     g.nchunks = vd::kChunks;
     g.scale = scale;
     if (g.packNum == 0) return VD_OK;
-    int dev = 0;
-    VD_HIP(hipGetDevice(&dev));
-    g.fair = fair_board(dev);
-    if (!g.fair) return fail(VD_ERR_NOMEM, "progress board allocation failed");
-    plan_split(g, options, dev);
+    g.fair = d->ds->board;
+    if (d->split) plan_split(g, options, d->ds);
     f(in_d, out_d, g, s);
     VD_HIP(hipGetLastError());
     return VD_OK;
@@ -336,8 +314,8 @@ int vd_num_chunks(void) { return vd::kChunks; }
 int vd_split_redecodes(int device, uint64_t* count)
 {
     if (!count) return fail(VD_ERR_ARG, "null argument");
-    SplitState* x = split_state(device);
-    if (!x) return fail(VD_ERR_DEVICE, "split bookkeeping unavailable");
+    DeviceState* x = device_state(device);
+    if (!x) return fail(VD_ERR_DEVICE, "per-device decode state unavailable");
     uint32_t v = 0;
     VD_HIP(hipMemcpy(&v, x->stats, 4, hipMemcpyDeviceToHost));
     *count = v;
@@ -365,6 +343,13 @@ int vd_create(int options, size_t preallocInputNum, int device, vd_decoder** out
     vd_decoder* d = new vd_decoder();
     d->options = options;
     d->device = device;
+    d->ds = device_state(device);
+    if (!d->ds) {
+        delete d;
+        return fail(VD_ERR_NOMEM, "per-device decode state allocation failed");
+    }
+    const char* nosplit = std::getenv("VD_NO_SPLIT");
+    d->split = !(nosplit && nosplit[0] == '1');
     if (hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreate(&d->ev0) != hipSuccess || hipEventCreate(&d->ev1) != hipSuccess) {
         vd_destroy(d);
@@ -407,7 +392,7 @@ int vd_run(vd_decoder* d, const void* input_h, void* output_h, size_t inputNum, 
     void* zout = zin ? mapped_host(output_h) : nullptr;
     if (zin && zout) {  // pinned host buffers: zero-copy decode (kernel_ms then includes the PCIe traffic)
         VD_HIP(hipEventRecord(d->ev0, d->stream));
-        int rc = launch_decode(d->options, zin, zout, inputNum, d->stream);
+        int rc = launch_decode(d, zin, zout, inputNum, d->stream);
         if (rc != VD_OK) return rc;
         VD_HIP(hipEventRecord(d->ev1, d->stream));
         VD_HIP(hipStreamSynchronize(d->stream));
@@ -418,7 +403,7 @@ int vd_run(vd_decoder* d, const void* input_h, void* output_h, size_t inputNum, 
     if (rc != VD_OK) return rc;
     VD_HIP(hipMemcpyAsync(d->in_d, input_h, inB, hipMemcpyHostToDevice, d->stream));
     VD_HIP(hipEventRecord(d->ev0, d->stream));
-    rc = launch_decode(d->options, d->in_d, d->out_d, inputNum, d->stream);
+    rc = launch_decode(d, d->in_d, d->out_d, inputNum, d->stream);
     if (rc != VD_OK) return rc;
     VD_HIP(hipEventRecord(d->ev1, d->stream));
     VD_HIP(hipMemcpyAsync(output_h, d->out_d, outB, hipMemcpyDeviceToHost, d->stream));
@@ -431,7 +416,7 @@ int vd_run_device(vd_decoder* d, const void* input_d, void* output_d, size_t inp
 {
     if (!d || !input_d || !output_d) return fail(VD_ERR_ARG, "null argument");
     if (message_len(d->options, inputNum) == 0) return fail(VD_ERR_ARG, "inputNum too small");
-    return launch_decode(d->options, input_d, output_d, inputNum, (hipStream_t)stream);
+    return launch_decode(d, input_d, output_d, inputNum, (hipStream_t)stream);
 }
 
 static int launch_pack(int options, const float* llr_d, size_t inputNum, float scale, void* packed_d, hipStream_t s)
@@ -471,9 +456,9 @@ int vd_run_device_llr(vd_decoder* d, const float* llr_d, void* output_d, size_t 
         if (rc != VD_OK) return rc;
         rc = launch_pack(d->options, llr_d, inputNum, scale, d->in_d, s);
         if (rc != VD_OK) return rc;
-        return launch_decode(d->options, d->in_d, output_d, inputNum, s);
+        return launch_decode(d, d->in_d, output_d, inputNum, s);
     }
-    return launch_decode(d->options, llr_d, output_d, inputNum, s, true, scale);
+    return launch_decode(d, llr_d, output_d, inputNum, s, true, scale);
 }
 
 int vd_run_llr(vd_decoder* d, const float* llr_h, void* output_h, size_t inputNum, float scale, float* kernel_ms)
@@ -534,7 +519,7 @@ int vd_run_stream(vd_decoder* d, const void* const* input_h, void* const* output
     if (zc) {
         auto t0 = std::chrono::steady_clock::now();
         for (int b = 0; b < nbatches; b++) {
-            int rc = launch_decode(d->options, mapped_host(input_h[b]), mapped_host(output_h[b]), inputNum, d->stream);
+            int rc = launch_decode(d, mapped_host(input_h[b]), mapped_host(output_h[b]), inputNum, d->stream);
             if (rc != VD_OK) return rc;
         }
         VD_HIP(hipStreamSynchronize(d->stream));
@@ -588,7 +573,7 @@ int vd_run_stream(vd_decoder* d, const void* const* input_h, void* const* output
             rc = fail(VD_ERR_DEVICE, "pipeline enqueue failed");
             break;
         }
-        rc = launch_decode(d->options, ins[k], outs[k], inputNum, d->stream);
+        rc = launch_decode(d, ins[k], outs[k], inputNum, d->stream);
         if (rc != VD_OK) break;
         if (hipEventRecord(decoded[k], d->stream) != hipSuccess) { rc = fail(VD_ERR_DEVICE, "record"); break; }
         if (b + 1 < nbatches && (rc = h2d(b + 1)) != VD_OK) break;
@@ -644,33 +629,6 @@ int vd_run_batches(int options, const void* const* input_h, void* const* output_
     for (int i = 0; i < ndev; i++)
         if (rcs[i] != VD_OK) return fail(rcs[i], errs[i]);
     if (wall_ms) *wall_ms = std::chrono::duration<float, std::milli>(t1 - t0).count();
-    return VD_OK;
-}
-
-int vd_synth_device(int options, size_t N, float snr, uint64_t seed, void* bits_d, void* packed_d, void* stream)
-{
-    if (!valid(options)) return fail(VD_ERR_OPTIONS, "options disabled by OptionsValid");
-    if (N % 16 || !packed_d) return fail(VD_ERR_ARG, "N must be a multiple of 16");
-    hipStream_t s = (hipStream_t)stream;
-    const float sigma = (float)std::pow(10.0, -(double)snr / 5.0);
-    const int noiseless = std::isinf(snr) && snr > 0 ? 1 : 0;
-    const uint64_t nval = 2 * (uint64_t)N;
-    const int per = ch_of(options) == 0 ? 32 : ch_of(options) == 1 ? 8 : ch_of(options) == 2 ? 4 : ch_of(options) == 3 ? 2 : 1;
-    const uint64_t nwords = nval / per;
-    const dim3 blk(256), grd((unsigned)((nwords + 255) / 256));
-    switch (ch_of(options)) {
-    case 0: hipLaunchKernelGGL(vd::synth_pack<0>, grd, blk, 0, s, seed, nval, sigma, noiseless, packed_d); break;
-    case 1: hipLaunchKernelGGL(vd::synth_pack<1>, grd, blk, 0, s, seed, nval, sigma, noiseless, packed_d); break;
-    case 2: hipLaunchKernelGGL(vd::synth_pack<2>, grd, blk, 0, s, seed, nval, sigma, noiseless, packed_d); break;
-    case 3: hipLaunchKernelGGL(vd::synth_pack<3>, grd, blk, 0, s, seed, nval, sigma, noiseless, packed_d); break;
-    case 4: hipLaunchKernelGGL(vd::synth_pack<4>, grd, blk, 0, s, seed, nval, sigma, noiseless, packed_d); break;
-    }
-    VD_HIP(hipGetLastError());
-    if (bits_d) {
-        hipLaunchKernelGGL(vd::synth_bits, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, s, seed, (uint64_t)N,
-                           (uint8_t*)bits_d);
-        VD_HIP(hipGetLastError());
-    }
     return VD_OK;
 }
 

@@ -197,10 +197,10 @@ __device__ __forceinline__ void tg_stage_lds(float& V, f2v e, float vp, bool upp
 // phase-0 bits (own-wins tag in the upper position half), which already are the decoded bits there.
 // One dependent LDS read per J stages instead of one per stage.
 template <int J, bool FIX5>
-__device__ __forceinline__ uint32_t traceback_word_tg(const char* ringb, uint32_t slot1, uint64_t k)
+__device__ __forceinline__ uint32_t traceback_word_tg(const char* ringb, uint32_t slot1, uint32_t k)
 {
     constexpr int G = 32 / J;
-    const int ph = (int)((2 * (k + 1)) % 6);  // stage phase of the emit block's first stage (even)
+    const int ph = (int)(2 * ((k + 1) % 3));  // stage phase of the emit block's first stage (even)
     // position of state T at a field end of stage phase s (odd) is rotl6(T, s) = (T*65 >> (6-s)) & 63
     int off[3];  // by s = (ph + c) % 6 for c = 1, 3, 5
     off[0] = 5 - ph;
@@ -374,21 +374,23 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t tg_rsrc(const void* in, uint64
 // 7-wave SIMDs set the kernel time.  In a split launch (Geom::nwhole) the first nwhole chunks are
 // decoded whole, one per wave, and each remaining chunk by one workgroup as kWaves pieces, so every
 // SIMD gets 6 whole chunks and one piece.  Piece 0 starts at the chunk start (exact).  Piece q > 0
-// starts kSplitWarm blocks before its first word's emit block from equal metrics and publishes its
-// renormalised metric vector at that block (split_publish); piece q-1 compares its own vector at the
-// same block (split_check).  Equal vectors mean every later decision of piece q equals the exact
-// decode's (the recursion and the tie rules depend only on metric differences; V at a block start is
-// VBASE + (metric - metric of position 0) * 2^S with cleared fields).  Piece 0 accepts pieces in order
-// while the checks passed (split_commit); otherwise it stops the pieces' output (cancel flag) and
-// re-decodes the whole chunk.  Block boundaries are multiples of 3 (the group length, 96 stages = 16
-// trellis periods) so both runs use the same position <-> state map there.  Flags carry the launch
-// epoch, so nothing is reset between launches; every wait is bounded (timeout = re-decode).  The
-// pieces of a chunk are the waves of one workgroup (one CU), so every flag and fence is workgroup-
-// scoped: an agent-scope release would write back the XCD's L2 at each flag.
-// flags[16] per split chunk: [q] spec ready (epoch), [4+q] check of boundary q (2 epoch + ok),
-// [8+q] piece q done (epoch), [12] cancel (epoch).
-constexpr int kSplitWarm = 6;      // warm-up blocks of a speculative piece (multiple of 3)
-constexpr int kSplitMinWords = 64; // chunks shorter than this are not split (host side)
+// starts kSplitWarm blocks before its first word's emit block from equal metrics; at that boundary
+// block it stores its renormalised metric vector (its start vector), and piece q-1 stores its own
+// vector at the same block (its end vector).  Equal vectors mean every later decision of piece q equals
+// the exact decode's (the recursion and the tie rules depend only on metric differences; V at a block
+// start is VBASE + (metric - metric of position 0) * 2^S with cleared fields), so piece q is verified
+// when piece q-1 is and the two vectors agree.  After each pass the workgroup synchronises (s_barrier)
+// and every wave evaluates the same checks.  Each unverified piece then re-decodes its words from its
+// boundary block, starting from the latest end vector of its left neighbour, and the checks repeat.  The
+// first unverified piece always restarts from an exact vector, so every pass verifies at least one more
+// piece: at most kWaves - 1 re-decode passes, no timeouts, no flags.  Writes of a later pass follow the
+// barrier, so the last (verified) decode of every word is the one that stays.  Block boundaries are
+// multiples of 3 (the group length, 96 stages = 16 trellis periods) so every run uses the same position
+// <-> state map there.  The pieces of a chunk are the waves of one workgroup (one CU), so all vectors are
+// exchanged through workgroup-visible global memory; nothing leaves the XCD's L2.
+constexpr int kSplitWarm = 6;                // warm-up blocks of a speculative piece (multiple of 3)
+constexpr int kSplitMinWords = 64;           // chunks shorter than this are not split (host side)
+constexpr int kSplitVecs = 3 * kWaves;       // per split chunk: start[q], end[parity 0][q], end[parity 1][q]
 struct SplitGeo {
     uint32_t s0, words, E;
     int Xspec, Xcmp;
@@ -399,6 +401,8 @@ __device__ __forceinline__ uint32_t split_bound(uint32_t Sc, int q)
     const uint32_t k = (uint32_t)q * Sc / kWaves;
     return k - (k + 1) % 3;
 }
+// piece q's frame: local word 0 = chunk word s0; it emits words [E, words) of the frame; Xspec / Xcmp:
+// the local blocks of its left / right boundary (-1: none)
 __device__ __forceinline__ SplitGeo split_geo(uint32_t Sc, int q)
 {
     SplitGeo g;
@@ -411,44 +415,14 @@ __device__ __forceinline__ SplitGeo split_geo(uint32_t Sc, int q)
     g.Xcmp = q == kWaves - 1 ? -1 : (int)(kn + 1 - g.s0);
     return g;
 }
-__device__ __forceinline__ void split_publish(uint32_t* flags, float* spec, int q, float V, int lane, uint32_t epoch)
+__device__ __forceinline__ int split_start_vec(int q) { return q; }
+__device__ __forceinline__ int split_end_vec(int q, uint32_t par) { return kWaves * (1 + (int)par) + q; }
+// both vectors equal in every lane (wave-uniform)
+__device__ __forceinline__ bool split_vec_eq(const float* vecs, int a, int b, int lane)
 {
-    spec[q * 64 + lane] = V;
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    if (lane == 0) __hip_atomic_store(flags + q, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-__device__ __forceinline__ bool split_check(uint32_t* flags, const float* spec, int q, float V, int lane, uint32_t epoch)
-{
-    const uint32_t f = __builtin_amdgcn_readfirstlane(
-        __hip_atomic_load(flags + q, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
-    if (f != epoch) return false;  // not published yet: treated as a mismatch
-    const float sv = __hip_atomic_load(spec + q * 64 + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    return __ballot(__builtin_bit_cast(uint32_t, sv) != __builtin_bit_cast(uint32_t, V)) == 0;
-}
-__device__ __forceinline__ void split_finish(uint32_t* flags, int q, bool cmpOk, int lane, uint32_t epoch)
-{
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");  // this piece's output words before its flags
-    if (lane == 0) {
-        if (q + 1 < kWaves) __hip_atomic_store(flags + 4 + q + 1, 2 * epoch + (cmpOk ? 1u : 0u), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-        __hip_atomic_store(flags + 8 + q, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-    }
-}
-// piece 0, after its own words: true iff every piece's start checked equal (waits, bounded, for the
-// pieces to finish: they run kSplitWarm blocks longer than piece 0)
-__device__ __forceinline__ bool split_commit(uint32_t* flags, bool cmp1, uint32_t epoch)
-{
-    if (!cmp1) return false;
-    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();  // 100 MHz
-    for (int q = 1; q < kWaves; q++) {
-        while (__builtin_amdgcn_readfirstlane(__hip_atomic_load(flags + 8 + q, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)) != epoch) {
-            if (__builtin_amdgcn_s_memrealtime() - t0 > 200000) return false;  // 2 ms: give up, re-decode
-            __builtin_amdgcn_s_sleep(4);
-        }
-        if (q + 1 < kWaves &&
-            __builtin_amdgcn_readfirstlane(__hip_atomic_load(flags + 4 + q + 1, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)) != 2 * epoch + 1)
-            return false;
-    }
-    return true;
+    const uint32_t x = __builtin_bit_cast(uint32_t, vecs[a * 64 + lane]);
+    const uint32_t y = __builtin_bit_cast(uint32_t, vecs[b * 64 + lane]);
+    return __ballot(x != y) == 0;
 }
 
 // ================================================================ tagged kernel: one chunk per wave
@@ -473,12 +447,11 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(7))
     const uint32_t chunk = split ? geo.nwhole + (blockIdx.x - geo.nwhole / kWaves) : blockIdx.x * kWaves + wv;
     const int piece = split ? wv : -1;
     const ChunkRange cr = chunk_range(geo, chunk);
-    if (cr.words == 0) return;
+    if (cr.words == 0) return;  // never in a split workgroup: split chunks have >= kSplitMinWords words
     const uint64_t t_clk0 = (ABL & 32) ? __builtin_amdgcn_s_memtime() : 0;
     const uint64_t t_rt0 = (ABL & 32) ? __builtin_amdgcn_s_memrealtime() : 0;
     const uint32_t Sc = OB == 32 ? cr.words : (cr.words + 1) / 2;  // 32-bit words traced back (chunk)
-    uint32_t* const sflags = split ? geo.flags + (size_t)(chunk - geo.nwhole) * 16 : nullptr;
-    float* const sspec = split ? geo.spec + (size_t)(chunk - geo.nwhole) * kWaves * 64 : nullptr;
+    float* const svec = split ? geo.spec + (size_t)(chunk - geo.nwhole) * kSplitVecs * 64 : nullptr;
 
     // per-lane LDS byte addresses of this position's table entries (row offsets are compile-time)
     // per-lane LDS byte offset of this position's entry in a phase-K row (row offsets are compile-time);
@@ -509,23 +482,21 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(7))
     // 2^(S-1) + h in (0, 2^S), so read-out and clearing are bit operations on the pattern.
     constexpr uint32_t VBASE = 0x4B400000u + (1u << (S - 1));  // pattern of 1.5*2^23 + 2^(S-1)
     const uint32_t fnm = ~((1u << S) - 1u), fhf = 1u << (S - 1);  // field clear: (p & fnm) | fhf
-    unsigned long long* fb = nullptr;
-    unsigned long long fret = 0;
-    uint32_t fadded = 0;
-    if constexpr (!(ABL & 256)) {
-        if (geo.fair) {
-            fb = geo.fair + simd_slot();
-            if (lane == 0) atomicAdd(fb, 1ull << 32);
-        }
-    }
+    Fair<(ABL & (1 << 20)) != 0> fair;  // fairness controller (vd_kernels.h; ABL & 256 disables)
+    if constexpr (!(ABL & 256)) fair.begin(geo.fair, lane);
     const uint64_t availB = IN::bytes(geo.availStages);
     const uint32_t vo1 = IN::voff(lane), vo2 = IN::voff((int)li);
+    // split workgroups (uniform bookkeeping): bit q of `verified` = piece q checked exact, bit q of
+    // `endpar` = which end-vector buffer holds piece q's latest end vector
+    uint32_t verified = 1u, endpar = 0u;
     for (int pass = 0;; pass++) {
-    // the words of this pass: [s0, s0 + Sw) of the chunk, written from word s0 + E on; Xspec / Xcmp:
-    // group-start blocks where a piece publishes / checks a metric vector (-1: none)
+    const bool runs = piece < 0 || !((verified >> piece) & 1u) || pass == 0;
+    if (runs) {
+    // the words of this run: [s0, s0 + Sw) of the chunk, written from word s0 + E on; Xspec / Xcmp: the
+    // group-start blocks of the piece's left / right boundary (-1: none)
     uint32_t s0 = 0, Sw = Sc, E = 0;
     int Xspec = -1, Xcmp = -1;
-    if (piece >= 0 && pass == 0) {
+    if (piece >= 0) {
         const SplitGeo sg = split_geo(Sc, piece);
         s0 = sg.s0;
         Sw = sg.words;
@@ -536,11 +507,17 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(7))
     const uint64_t wOut = cr.startWord + s0;  // output word of local word 0 (OB == 32 when split)
     const uint64_t start = wOut * OB;
     const uint32_t nblk = Sw + 2;
-    bool cmpOk = false;
     float V = __builtin_bit_cast(float, VBASE);
+    // a re-decode starts at the piece's boundary block from its left neighbour's latest end vector
+    const uint32_t j0 = pass == 0 ? 0u : (uint32_t)Xspec;
+    if (pass > 0) {  // piece >= 1 here (piece 0 is exact and never re-decodes)
+        const int pl = piece > 0 ? piece - 1 : 0;
+        V = svec[split_end_vec(pl, (endpar >> pl) & 1u) * 64 + lane];
+        svec[split_start_vec(piece) * 64 + lane] = V;
+    }
     uint32_t kb = 0;
-    uint32_t tbn = TBS - 3 * (blockIdx.x & 3);
-    __amdgpu_buffer_rsrc_t rs = tg_rsrc<CH>(in, start, availB);
+    uint32_t tbn = pass == 0 ? TBS - 3 * (blockIdx.x & 3) : TBS;
+    __amdgpu_buffer_rsrc_t rs = tg_rsrc<CH>(in, start + 32ull * j0, availB);
     typename IN::raw_t rA = IN::template load<0>(rs, vo1);  // stage `lane` of the group
     typename IN::raw_t rB = IN::template load<2>(rs, vo2);  // stage 64 + li
 
@@ -623,11 +600,8 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(7))
         if (j >= 2 && (j - 1 - kb == tbn || j == nblk - 1)) {
             wave_sync();
             const uint32_t nw = j - 1 - kb;
-            // a speculative piece stops writing once its chunk is being re-decoded (cancel flag)
-            const bool cancelled = piece > 0 && pass == 0 &&
-                                   __hip_atomic_load(sflags + 12, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == geo.epoch;
-            if (!(ABL & 1) && (uint32_t)lane < nw && kb + lane >= E && !cancelled) {
-                const uint64_t k = kb + lane;
+            if (!(ABL & 1) && (uint32_t)lane < nw && kb + lane >= E) {
+                const uint32_t k = kb + (uint32_t)lane;
                 const uint32_t Q0 = (uint32_t)(wv * (TBS + 1) * 256 + (lane + 1) * 256);
                 uint32_t w = traceback_word_tg<J, CORE == B32>((const char*)ring_all, Q0, k);
                 if constexpr (OB == 32) {
@@ -672,9 +646,9 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(7))
         }
     };
     const int r6a = lane % 6, r6b = (int)(li + 64) % 6;
-    for (uint32_t j = 0;; j += 3) {
+    for (uint32_t j = j0;; j += 3) {
         // group head: the table from the inputs loaded one group ago, the next group's loads, then the
-        // fairness board (its atomic returns during this group; nothing here waits on it)
+        // fairness board (its load returns during this group; nothing here waits on it)
         if constexpr (!(ABL & 8)) {  // ABL 8 (tools only): no table build
             int A, B;
             IN::ab(rA, lane, A, B, geo.scale);
@@ -689,24 +663,9 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(7))
             rA = IN::template load<0>(rs, vo1);
             rB = IN::template load<2>(rs, vo2);
         }
-        if constexpr (!(ABL & 256)) {
-            if (fb) {
-                if (j > 0) {
-                    const uint64_t r = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(fret >> 32)) << 32) |
-                                       (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)fret);
-                    const int64_t n = (int64_t)(r >> 32), sum = (int64_t)(uint32_t)r + 3;
-                    const int64_t d = (int64_t)j * n - sum;
-                    if (d <= -3 * n) __builtin_amdgcn_s_setprio(3);
-                    else if (d <= 0) __builtin_amdgcn_s_setprio(2);
-                    else if (d <= 3 * n) __builtin_amdgcn_s_setprio(1);
-                    else __builtin_amdgcn_s_setprio(0);
-                }
-                if (lane == 0) fret = atomicAdd(fb, 3ull);
-                fadded += 3;
-            }
-        }
-        if (split && (int)j == Xspec) split_publish(sflags, sspec, piece, V, lane, geo.epoch);
-        if (split && (int)j == Xcmp) cmpOk = split_check(sflags, sspec, piece + 1, V, lane, geo.epoch);
+        if constexpr (!(ABL & 256)) fair.group(j, lane);
+        if (split && pass == 0 && (int)j == Xspec) svec[split_start_vec(piece) * 64 + lane] = V;
+        if (split && (int)j == Xcmp) svec[split_end_vec(piece, (uint32_t)pass & 1u) * 64 + lane] = V;
         wave_sync();
         sfor<TGD>([&](auto X) { issue(X); });
         if (!block(std::integral_constant<int, 0>{}, j)) break;
@@ -714,21 +673,21 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(7))
         if (!block(std::integral_constant<int, 4>{}, j + 2)) break;
         wave_sync();
     }
-    if (piece < 0 || pass > 0) break;
-    if (piece > 0) {  // speculative piece: record the check of the next boundary, then done
-        split_finish(sflags, piece, cmpOk, lane, geo.epoch);
-        break;
-    }
-    // piece 0: its start is exact; accept the pieces in order while each boundary check passed
-    if (split_commit(sflags, cmpOk, geo.epoch)) break;
-    if (lane == 0) {  // otherwise re-decode the whole chunk (pass 1) after stopping the pieces' writes
-        __hip_atomic_store(sflags + 12, geo.epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-        if (geo.stats) atomicAdd(geo.stats, 1u);
-    }
+    }  // runs
+    if (piece < 0) break;
+    // split workgroup: evaluate the boundary checks (every wave the same), then re-decode what failed
+    const uint32_t ran = pass == 0 ? (1u << kWaves) - 1u : ~verified & ((1u << kWaves) - 1u);
+    endpar = (endpar & ~ran) | ((pass & 1) ? ran : 0u);
+    __syncthreads();
+    for (int q = 1; q < kWaves; q++)
+        if (!((verified >> q) & 1u) && ((verified >> (q - 1)) & 1u) &&
+            split_vec_eq(svec, split_start_vec(q), split_end_vec(q - 1, (endpar >> (q - 1)) & 1u), lane))
+            verified |= 1u << q;
+    if (verified == (1u << kWaves) - 1u) break;
+    if (lane == 0 && !((verified >> piece) & 1u) && geo.stats) atomicAdd(geo.stats, 1u);
+    __syncthreads();  // the next pass overwrites vectors read above
     }  // pass
-    if constexpr (!(ABL & 256)) {
-        if (fb && lane == 0) atomicAdd(fb, 0ull - ((1ull << 32) + fadded));
-    }
+    if constexpr (!(ABL & 256)) fair.end(lane);
     if constexpr (ABL & 32) {
         const uint64_t c1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
         if (lane == 0) {

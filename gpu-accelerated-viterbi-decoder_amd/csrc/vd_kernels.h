@@ -9,14 +9,14 @@
 //    of every stage pairs lanes p and p^(1<<q), q = (t%6+5)%6, so each stage needs one xor-lane
 //    exchange: DPP quad_perm (q=0,1), DPP row_half_mirror+quad_perm (q=2), DPP row_ror:8 (q=3),
 //    ds_swizzle xor-16 (q=4), ds_bpermute xor-32 (q=5).
-//  * Metric cores.  int32 (M_B32): one stream chunk per wave.  int16x2 (M_B16) and fp16x2 (M_FP16):
-//    two chunks per wave, chunk 2w in the low and chunk 2w+1 in the high half of every lane, so one
-//    v_pk_add/v_pk_sub/v_pk_max advances two chunks.
+//  * Metric cores.  Every core (M_B32, M_B16, M_FP16) runs in exact-integer fp32, one chunk per wave;
+//    the metric type only selects the tie rule (see "fp32 core" below).  This file holds the shared
+//    helpers and vd_decode_sc, the untagged kernel that SOFT16 uses; vd_kernel_tg.h holds the tagged
+//    kernel every other input format uses.
 //  * Survivors.  No register exchange: each stage's decision ("took the exchanged predecessor") is
-//    the sign bit of a candidate difference, shifted into per-lane words with pure-VGPR ops; one
-//    word per lane per 32-stage block (int32) or per 16-stage half-block (packed) goes to an LDS ring.
-//    Output words are traced back lane-parallel (TB words at a time) in POSITION space, where a
-//    traceback step is p ^= d << q -- no state arithmetic.
+//    the sign bit of a candidate difference, accumulated into one word per lane per 32-stage block
+//    that goes to an LDS ring.  Output words are traced back lane-parallel (TB words at a time) in
+//    POSITION space, where a traceback step is p ^= d << q -- no state arithmetic.
 //  * Branch metrics.  Per 32-stage block, 32 lanes compute the 4 branch metrics of one stage each
 //    into an LDS table; every stage each lane reads the metric of its own transition with one
 //    ds_read_b32 whose base register depends only on (lane, t%6).
@@ -35,26 +35,28 @@ enum Ch : int { HARD = 0, SOFT4 = 1, SOFT8 = 2, SOFT16 = 3, FP32 = 4 };
 enum Core : int { B32 = 0, B16 = 1, F16 = 2 };
 
 constexpr int kChunks = 6400;  // reference blocksNum_total = 16*400 (viterbi.cu:19)
-constexpr int kTB = 16;        // output words traced back per batch (packed kernel)
 constexpr int kTBsc = 14;      // fp32 kernel: 14 words per batch keeps 7 four-wave workgroups per CU
 
 struct Geom {
     uint64_t packNum;      // output words of bpp bits (getMessageLen / bpp)
     uint64_t availStages;  // stages readable from the input buffer
     uint32_t nchunks;
-    unsigned long long* fair;  // per-SIMD progress board (kFairSlots words, zero at rest) or null
-    float scale;               // LLR input (channel ids 8 + base): SoftDecisionPacker scale, else unused
+    uint32_t* fair;        // per-SIMD progress board (kFairBoardWords, empty at rest) or null
+    float scale;           // LLR input (channel ids 8 + base): SoftDecisionPacker scale, else unused
     // split launch (vd_kernel_tg.h "split chunks"): chunks >= nwhole are decoded as kWaves pieces, one
     // workgroup each; 0 = every chunk whole
     uint32_t nwhole = 0;
-    uint32_t epoch = 0;          // launch id carried by the split flags
-    float* spec = nullptr;       // [chunk - nwhole][kWaves][64] published metric vectors
-    uint32_t* flags = nullptr;   // [chunk - nwhole][16] split flags
-    uint32_t* stats = nullptr;   // count of split chunks re-decoded whole (or null)
+    float* spec = nullptr;       // [chunk - nwhole][kSplitVecs][64] piece boundary metric vectors
+    uint32_t* stats = nullptr;   // count of split pieces re-decoded (or null)
 };
-// progress board: one 64-bit word per SIMD slot, (waves << 32) + blocks started; indexed by
-// (XCC, SE, SH, CU, SIMD) from the hardware wave id.  Only issue priority depends on it.
+// Progress board of the fairness controller: per SIMD slot (XCC, SE, SH, CU, SIMD from the hardware
+// wave id) kFairWaves 32-bit words, one per hardware wave slot of that SIMD (HW_ID.WAVE_ID): the blocks
+// the wave in that slot has started, kFairEmpty when the slot is free.  Only issue priority depends on
+// it; a collision (another kernel on the same SIMD) only perturbs priorities.
 constexpr int kFairSlots = 8 * 8 * 2 * 16 * 4;
+constexpr int kFairWaves = 16;
+constexpr size_t kFairBoardWords = (size_t)kFairSlots * kFairWaves;
+constexpr uint32_t kFairEmpty = 0xFFFFFFFFu;
 
 // ---------------------------------------------------------------- compile-time loop helper
 template <typename F, int... I>
@@ -209,48 +211,6 @@ __device__ __forceinline__ ChunkRange chunk_range(const Geom& g, uint32_t c)
     return r;
 }
 
-// ---------------------------------------------------------------- lane-parallel traceback
-// Lane traces output word k (0-based within its chunk); block k+2 sits in ring slot l+1, block k+1
-// in slot l.  Position-space traceback: p_{t-1} = p_t ^ (d_t(p_t) << q_t); the decoded bit of stage t
-// is bit q_t of p_{t-1} (the dropped bit of the predecessor state).  Reference: viterbiTB.cuh:4-21.
-// Ring formats:
-//   PK=false (int32 core): slot = 64 words (lane p), bit 31-s = decision of stage s of the block.
-//   PK=true  (packed cores): slot = 2 half-blocks x 64 words; half-block hb holds stages 16hb..16hb+15,
-//            the low 16 bits for the chunk in the low metric halves, the high 16 bits for the other;
-//            bit s' of a 16-bit half = stage 16hb+s'.  `Q` carries 2h (byte select of the half).
-template <bool PK>
-__device__ __forceinline__ uint32_t traceback_word(const char* ring, int h, int l, uint64_t k)
-{
-    constexpr int SLOTB = PK ? 512 : 256;
-    const int e6 = (int)((95 + 32 * k) % 6);  // stage phase of the traceback start
-    int MK[6], QS[6];
-    sfor<6>([&](auto R) {
-        constexpr int r = decltype(R)::value;
-        int t6 = (e6 - r + 6) % 6;
-        int q = (t6 + 5) % 6;
-        MK[r] = 4 << q;
-        QS[r] = q + 2;
-    });
-    uint32_t Q = (uint32_t)((l + 1) * SLOTB + (PK ? 2 * h : 0));  // position 0 = state 0
-    uint32_t word = 0;
-    sfor<64>([&](auto I) {
-        constexpr int i = decltype(I)::value;
-        constexpr int s = 31 - (i & 31);  // stage within the block
-        int d;
-        if constexpr (PK) {
-            constexpr int off = (s >> 4) * 256;
-            uint32_t w = *(const uint16_t*)(ring + Q + off);
-            d = (int)(w << (31 - (s & 15))) >> 31;
-        } else {
-            uint32_t w = *(const uint32_t*)(ring + Q);
-            d = (int)(w << s) >> 31;
-        }
-        Q ^= (uint32_t)(d & MK[i % 6]);
-        if constexpr (i == 31) Q -= (uint32_t)SLOTB;
-        if constexpr (i >= 32) word |= ((Q >> QS[i % 6]) & 1u) << (i - 32);  // word bit <-> stage 63+32k-(i-32)
-    });
-    return word;
-}
 
 // ---------------------------------------------------------------- traceback, fp32 kernel ring format
 // ring: per block slot 64 words (lane p), bit 31-s = take-bit of stage s.  `Q` is a byte offset from
@@ -414,6 +374,60 @@ __device__ __forceinline__ uint32_t simd_slot()
     const uint32_t x = __builtin_amdgcn_s_getreg(20 | (0 << 6) | (31 << 11)) & 7u;  // XCC_ID
     return (((x * 8 + ((h >> 13) & 7u)) * 2 + ((h >> 12) & 1u)) * 16 + ((h >> 8) & 15u)) * 4 + ((h >> 4) & 3u);
 }
+
+// Fairness controller.  The SIMD arbiter favours the oldest wave, so left alone the waves sharing a
+// SIMD finish up to 2x apart and the tail of the launch runs at low occupancy (tools/vd_ablate clock
+// stamps).  At every 3-block group head each wave posts the blocks it has started to its own board word
+// and sets its issue priority from its lag behind the mean of the SIMD's waves, read at the previous
+// head.  Posting is a plain store and reading one 64-byte load (16 lanes): both stay in the XCD's L2
+// (all waves of a SIMD are on one XCD), so the board adds no HBM or fabric traffic -- a returning atomic
+// per group went past the L2 and cost 11 MB of writes per launch (profiles/r02).  LD1: read with
+// agent-scope (sc1) loads instead of workgroup-scope (sc0) ones (tools, A/B).
+template <bool LD1 = false>
+struct Fair {
+    uint32_t* mine = nullptr;   // this wave's word
+    uint32_t* simd = nullptr;   // the SIMD's kFairWaves words
+    uint32_t seen = kFairEmpty; // lane l < kFairWaves: word l as read at the previous group head
+
+    __device__ __forceinline__ void begin(uint32_t* board, int lane)
+    {
+        if (!board) return;
+        const uint32_t wid = __builtin_amdgcn_s_getreg(4 | (0 << 6) | (31 << 11)) & (kFairWaves - 1);
+        simd = board + (size_t)simd_slot() * kFairWaves;
+        mine = simd + wid;
+        if (lane == 0) __hip_atomic_store(mine, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+    }
+    // group head; j = blocks started so far (a multiple of 3)
+    __device__ __forceinline__ void group(uint32_t j, int lane)
+    {
+        if (!mine) return;
+        if (j > 0) {
+            const bool act = lane < kFairWaves && seen != kFairEmpty;
+            const uint32_t n = (uint32_t)__builtin_popcountll(__ballot(act));
+            uint32_t x = act ? seen : 0u;
+            // sum of the 16 words: row_shr 1, 2, 4, 8 (lanes past the row edge add 0); lane 15 holds it
+            x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, true);
+            x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xF, 0xF, true);
+            x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xF, 0xF, true);
+            x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xF, 0xF, true);
+            const uint32_t sum = (uint32_t)__builtin_amdgcn_readlane((int)x, 15);
+            // (own - mean) * n in blocks; own word read back as posted at the previous head (j - 3)
+            const int64_t d = (int64_t)(j - 3) * n - (int64_t)sum;
+            if (d <= -3 * (int64_t)n) __builtin_amdgcn_s_setprio(3);
+            else if (d <= 0) __builtin_amdgcn_s_setprio(2);
+            else if (d <= 3 * (int64_t)n) __builtin_amdgcn_s_setprio(1);
+            else __builtin_amdgcn_s_setprio(0);
+        }
+        if (lane == 0) __hip_atomic_store(mine, j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+        const uint32_t* w = simd + (lane & (kFairWaves - 1));
+        if constexpr (LD1) seen = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        else seen = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    __device__ __forceinline__ void end(int lane)
+    {
+        if (mine && lane == 0) __hip_atomic_store(mine, kFairEmpty, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+    }
+};
 template <int CH, int CORE, int OB, int ABL = 0>
 __global__ __launch_bounds__(64 * kWaves) void vd_decode_sc(const void* __restrict__ in, void* __restrict__ out, Geom geo)
 {
@@ -448,19 +462,9 @@ __global__ __launch_bounds__(64 * kWaves) void vd_decode_sc(const void* __restri
 
     float pm = 0.0f;
     uint32_t kb = 0;
-    // Fairness: the SIMD arbiter favours the oldest wave, so left alone the waves sharing a SIMD
-    // finish up to 2x apart and the tail runs at low occupancy (tools/vd_ablate clock stamps).
-    // Each wave posts its progress to the SIMD's board word at every 3-block group and sets its
-    // issue priority from its lag behind the SIMD mean (ABL & 256 disables).
-    unsigned long long* fb = nullptr;
-    unsigned long long fret = 0;
-    uint32_t fadded = 0;
-    if constexpr (!(ABL & 256)) {
-        if (geo.fair) {
-            fb = geo.fair + simd_slot();
-            if (lane == 0) atomicAdd(fb, 1ull << 32);
-        }
-    }
+    // fairness controller (see Fair; ABL & 256 disables)
+    Fair<> fair;
+    if constexpr (!(ABL & 256)) fair.begin(geo.fair, lane);
     // first traceback batch is shortened per workgroup so the waves sharing a SIMD do not all enter
     // their latency-bound traceback in the same block
     uint32_t tbn = TBS - 3 * (blockIdx.x & 3);
@@ -526,23 +530,7 @@ __global__ __launch_bounds__(64 * kWaves) void vd_decode_sc(const void* __restri
         return j + 1 < nblk;
     };
     for (uint32_t j = 0;; j += 3) {
-        if constexpr (!(ABL & 256)) {
-            if (fb) {
-                if (j > 0) {
-                    // board value returned at the previous group head (own add of 3 not included)
-                    const uint64_t r = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(fret >> 32)) << 32) |
-                                       (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)fret);
-                    const int64_t n = (int64_t)(r >> 32), sum = (int64_t)(uint32_t)r + 3;
-                    const int64_t d = (int64_t)j * n - sum;  // (own - mean) * n, in blocks
-                    if (d <= -3 * n) __builtin_amdgcn_s_setprio(3);
-                    else if (d <= 0) __builtin_amdgcn_s_setprio(2);
-                    else if (d <= 3 * n) __builtin_amdgcn_s_setprio(1);
-                    else __builtin_amdgcn_s_setprio(0);
-                }
-                if (lane == 0) fret = atomicAdd(fb, 3ull);
-                fadded += 3;
-            }
-        }
+        if constexpr (!(ABL & 256)) fair.group(j, lane);
         if (lane < 32) {
             int A, B;
             IN::ab(rA, start + 32ull * j + li, avail, A, B);
@@ -564,9 +552,7 @@ __global__ __launch_bounds__(64 * kWaves) void vd_decode_sc(const void* __restri
         wave_sync();  // this group's table reads complete before the next group overwrites it
     }
     if constexpr (ABL & 8) asm volatile("" ::"v"(pm));
-    if constexpr (!(ABL & 256)) {
-        if (fb && lane == 0) atomicAdd(fb, 0ull - ((1ull << 32) + fadded));  // board back to zero
-    }
+    if constexpr (!(ABL & 256)) fair.end(lane);  // slot free again
     if constexpr (ABL & 32) {
         const uint64_t c1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
         if (lane == 0) {
@@ -578,139 +564,5 @@ __global__ __launch_bounds__(64 * kWaves) void vd_decode_sc(const void* __restri
     }
 }
 
-// ================================================================ packed cores: two chunks per wave
-template <int CORE>
-struct Pk;
-template <>
-struct Pk<B16> {
-    typedef short v2 __attribute__((ext_vector_type(2)));
-    static constexpr bool kInvert = true;  // sign(t2 - t1) = NOT take: exchanged wins ties
-    static __device__ __forceinline__ uint32_t cvt(int a) { return (uint32_t)(uint16_t)(int16_t)a; }
-    static __device__ __forceinline__ v2 as(uint32_t x) { return __builtin_bit_cast(v2, x); }
-    static __device__ __forceinline__ uint32_t bits(v2 x) { return __builtin_bit_cast(uint32_t, x); }
-    // one ACS for both halves (viterbiACS.cuh:113-119,216-220); d carries the decision in the sign bits
-    static __device__ __forceinline__ uint32_t acs(uint32_t own, uint32_t oth, uint32_t m, uint32_t& d)
-    {
-        v2 t1 = as(own) + as(m), t2 = as(oth) - as(m);
-        d = bits(t2 - t1);
-        return bits(__builtin_elementwise_max(t1, t2));
-    }
-    static __device__ __forceinline__ uint32_t sub(uint32_t a, uint32_t b) { return bits(as(a) - as(b)); }
-};
-template <>
-struct Pk<F16> {
-    typedef _Float16 v2 __attribute__((ext_vector_type(2)));
-    static constexpr bool kInvert = false;  // sign(t1 - t2) = take: own wins ties (__hlt2_mask is strict)
-    static __device__ __forceinline__ uint32_t cvt(int a) { return (uint32_t)__builtin_bit_cast(uint16_t, (_Float16)a); }
-    static __device__ __forceinline__ v2 as(uint32_t x) { return __builtin_bit_cast(v2, x); }
-    static __device__ __forceinline__ uint32_t bits(v2 x) { return __builtin_bit_cast(uint32_t, x); }
-    // viterbiACS.cuh:147-157,250-256; metrics stay exact integers below 2048 in magnitude
-    static __device__ __forceinline__ uint32_t acs(uint32_t own, uint32_t oth, uint32_t m, uint32_t& d)
-    {
-        v2 t1 = as(own) + as(m), t2 = as(oth) - as(m);
-        d = bits(t1 - t2);
-        return bits(__builtin_elementwise_max(t1, t2));
-    }
-    static __device__ __forceinline__ uint32_t sub(uint32_t a, uint32_t b) { return bits(as(a) - as(b)); }
-};
-// shift both halves right by one and insert the two sign bits of d at bits 15 and 31
-__device__ __forceinline__ uint32_t pk_push(uint32_t acc, uint32_t d)
-{
-    typedef unsigned short u2 __attribute__((ext_vector_type(2)));
-    uint32_t sh = __builtin_bit_cast(uint32_t, __builtin_bit_cast(u2, acc) >> (u2){1, 1});
-    return (d & 0x80008000u) | (sh & 0x7FFF7FFFu);
-}
-
-template <int CH, int CORE, int OB, int ABL = 0>
-__global__ __launch_bounds__(64) void vd_decode_pk(const void* __restrict__ in, void* __restrict__ out, Geom geo)
-{
-    using IN = In<CH>;
-    using P = Pk<CORE>;
-    __shared__ uint4 tab[32];                     // per stage: BM[0..3] as (chunk lo, chunk hi) pairs
-    __shared__ uint32_t ring[(kTB + 1) * 128];    // per block: 64 words chunk lo, 64 words chunk hi
-    const int lane = threadIdx.x;
-    const int half = lane >> 5, li = lane & 31;
-    const ChunkRange c0 = chunk_range(geo, 2 * blockIdx.x), c1 = chunk_range(geo, 2 * blockIdx.x + 1);
-    if (c0.words == 0 && c1.words == 0) return;
-    const ChunkRange my = half ? c1 : c0;
-    const uint32_t S0 = OB == 32 ? c0.words : (c0.words + 1) / 2;
-    const uint32_t S1 = OB == 32 ? c1.words : (c1.words + 1) / 2;
-    const uint32_t Smy = half ? S1 : S0;
-    const uint32_t nblk = (S0 > S1 ? S0 : S1) + 2;
-    const uint64_t start = my.startWord * OB;
-    const uint64_t avail = my.words ? geo.availStages : 0;  // an empty chunk reads nothing
-
-    int L4[6];
-    sfor<6>([&](auto K) {
-        constexpr int k = decltype(K)::value;
-        L4[k] = own_label(lane, k) * 4;
-    });
-    const int bp_addr = (lane ^ 32) * 4;
-    const uint32_t* tabu = (const uint32_t*)tab;
-
-    uint32_t pm = 0, acc = 0, accLo = 0;
-    uint32_t kb = 0;
-    typename IN::raw_t raw = IN::load(in, start + (uint64_t)li, avail);
-
-    for (uint32_t j = 0; j < nblk; j++) {
-        {
-            int A, B;
-            IN::ab(raw, start + 32ull * j + li, avail, A, B);
-            uint32_t a = P::cvt(A), b = P::cvt(B), na = P::cvt(-A), nb = P::cvt(-B);
-            uint32_t pa = __shfl_xor(a, 32), pb = __shfl_xor(b, 32), pna = __shfl_xor(na, 32), pnb = __shfl_xor(nb, 32);
-            if (half == 0)
-                tab[li] = make_uint4(na | (pna << 16), nb | (pnb << 16), b | (pb << 16), a | (pa << 16));
-        }
-        if (j + 1 < nblk) raw = IN::load(in, start + 32ull * (j + 1) + (uint64_t)li, avail);
-        __syncthreads();
-
-        auto run = [&](auto PHc) {
-            constexpr int PH = decltype(PHc)::value;
-            sfor<32>([&](auto I) {
-                constexpr int i = decltype(I)::value;
-                constexpr int K = (PH + i) % 6;
-                constexpr int Q = (K + 5) % 6;
-                const uint32_t m = (ABL & 4) ? (uint32_t)L4[K] : tabu[i * 4 + (L4[K] >> 2)];
-                const uint32_t oth = (uint32_t)xchg<Q, ABL>((int)pm, bp_addr);
-                uint32_t d;
-                pm = P::acs(pm, oth, m, d);
-                if constexpr (!(ABL & 8)) acc = pk_push(acc, d);
-                if constexpr (i == 15) accLo = acc;  // first half-block complete
-            });
-        };
-        switch (j % 3) {
-        case 0: run(std::integral_constant<int, 0>{}); break;
-        case 1: run(std::integral_constant<int, 2>{}); break;
-        default: run(std::integral_constant<int, 4>{}); break;
-        }
-        // decision-neutral renormalisation of both halves by the metric of position 0
-        pm = P::sub(pm, __builtin_amdgcn_readfirstlane(pm));
-        __syncthreads();
-        if (j >= 1) {
-            ring[(j - 1 - kb) * 128 + lane] = P::kInvert ? ~accLo : accLo;
-            ring[(j - 1 - kb) * 128 + 64 + lane] = P::kInvert ? ~acc : acc;
-        }
-        if (j >= 2 && (j - 1 - kb == (uint32_t)kTB || j == nblk - 1)) {
-            __syncthreads();
-            const uint32_t hi = (j - 1) < Smy ? (j - 1) : Smy;  // words kb .. min(j-1,S)-1 of my chunk
-            const uint32_t nw = hi > kb ? hi - kb : 0;
-            if (!(ABL & 1) && (uint32_t)li < nw) {
-                const uint64_t k = kb + li;
-                uint32_t w = traceback_word<true>((const char*)ring, half, li, k);
-                if constexpr (OB == 32) {
-                    ((uint32_t*)out)[my.startWord + k] = w;
-                } else {
-                    uint16_t* o = (uint16_t*)out + my.startWord;
-                    o[2 * k] = (uint16_t)(w >> 16);
-                    if (2 * k + 1 < my.words) o[2 * k + 1] = (uint16_t)(w & 0xFFFF);
-                }
-            }
-            __syncthreads();
-            ring[lane] = P::kInvert ? ~accLo : accLo;
-            ring[64 + lane] = P::kInvert ? ~acc : acc;
-            kb = j - 1;
-        }
-    }
-}
 
 }  // namespace vd

@@ -117,7 +117,10 @@ private:
         const long lo = cfg_ == SOFT4 ? -8 : cfg_ == SOFT8 ? -128 : -32768;
         const long hi = -lo - 1;
         const uint32_t mask = cfg_ == SOFT4 ? 0xFu : cfg_ == SOFT8 ? 0xFFu : 0xFFFFu;
+        // SOFT4/SOFT8 narrow lrintf's long to int BEFORE saturating, SOFT16 saturates the long
+        // (reference viterbiDF.h:108,114 vs :120): |v| >= 2^31 quantises differently
         long q = std::lrintf(v);
+        if (cfg_ != SOFT16) q = (long)(int)q;
         q = q < lo ? lo : (q > hi ? hi : q);
         return (uint32_t)q & mask;
     }

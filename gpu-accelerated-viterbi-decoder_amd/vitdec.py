@@ -6,7 +6,7 @@ bitsPerPack, encDataPerPack, ...), the same size helpers and the same `run(input
 call returning the kernel time in ms.  Errors raise VitdecError (the reference exits the process,
 gpuerrors.h:8-17; the C++ header include/viterbi.h keeps that behaviour).
 
-Device-side entry points (`run_device`, `synth_device`) take raw device pointers, e.g.
+Device-side entry points (`run_device`, `simulate_device`) take raw device pointers, e.g.
 `tensor.data_ptr()` of a torch tensor on the decoder's device, and a HIP stream handle
 (`torch.cuda.current_stream().cuda_stream`).  torch is only plumbing for memory and streams.
 
@@ -39,7 +39,7 @@ _ERRNAMES = {-1: "VD_ERR_OPTIONS", -2: "VD_ERR_ARG", -3: "VD_ERR_DEVICE", -4: "V
 
 # every entry point declared in include/vd_capi.h (tests check the library exports all of them)
 EXPORTS = ["vd_options_valid", "vd_input_size", "vd_message_len", "vd_output_size", "vd_num_chunks",
-           "vd_create", "vd_destroy", "vd_run", "vd_run_device", "vd_run_batches", "vd_synth_device",
+           "vd_create", "vd_destroy", "vd_run", "vd_run_device", "vd_run_batches",
            "vd_simulate_host", "vd_count_errors", "vd_last_error", "vd_device_count", "vd_kernel_name",
            "vd_pack_device", "vd_run_device_llr", "vd_run_llr", "vd_host_alloc", "vd_host_free",
            "vd_run_stream", "vd_channel_device", "vd_simulate_device", "vd_mt_state_after", "vd_split_redecodes"]
@@ -71,7 +71,6 @@ def lib():
     L.vd_run_device.argtypes = [vp, vp, vp, sz, vp]
     L.vd_run_batches.argtypes = [i, ctypes.POINTER(vp), ctypes.POINTER(vp), sz, i, ctypes.POINTER(i), i,
                                  ctypes.POINTER(f)]
-    L.vd_synth_device.argtypes = [i, sz, f, ctypes.c_uint64, vp, vp, vp]
     L.vd_simulate_host.argtypes = [i, sz, f, ctypes.c_uint32, ctypes.c_uint32, vp, vp]
     L.vd_channel_device.argtypes = [sz, f, ctypes.c_uint32, ctypes.c_uint32, vp, vp, vp]
     L.vd_simulate_device.argtypes = [i, sz, f, ctypes.c_uint32, ctypes.c_uint32, vp, vp, vp]
@@ -257,12 +256,6 @@ def pack_device(options, llr_ptr, inputNum, packed_ptr, scale=40000.0, stream=0)
     """The reference's SoftDecisionPacker on device floats -> vd_input_size(options, inputNum) bytes."""
     _check(lib().vd_pack_device(options, ctypes.c_void_p(llr_ptr), inputNum, scale, ctypes.c_void_p(packed_ptr),
                                 ctypes.c_void_p(stream)))
-
-
-def synth_device(options, n_bits, snr, seed, bits_ptr, packed_ptr, stream=0):
-    """GPU synthetic source: N-bit message -> packed channel input in device memory."""
-    _check(lib().vd_synth_device(options, n_bits, snr, seed, ctypes.c_void_p(bits_ptr) if bits_ptr else None,
-                                 ctypes.c_void_p(packed_ptr), ctypes.c_void_p(stream)))
 
 
 def simulate_host(options, n_bits, snr, bit_seed, noise_seed):

@@ -113,16 +113,8 @@ int vd_run_device_llr(vd_decoder* dec, const float* llr_d, void* output_d, size_
 /* Blocking host-to-host variant (H2D of the floats, fused decode, D2H); kernel_ms as in vd_run. */
 int vd_run_llr(vd_decoder* dec, const float* llr_h, void* output_h, size_t inputNum, float scale, float* kernel_ms);
 
-/* ---- synthetic channel source on the GPU (the reference's RandBitGen | ConvolutionalEncoder |
- *      AddNoise | SoftDecisionPacker chain, viterbiDF.h:20-167, is host-side; this is the
- *      product's own device-resident generator for benchmarks: bits from a counter-based hash,
- *      not the reference's mt19937 stream) ---- */
-
-/* Fill bits_d (N bytes, 0/1) and the packed channel input packed_d (vd_input_size(options, 2N)
- * bytes) for an N-bit message at `snr` (reference scaling: sigma = 10^(-snr/5), quantiser scale
- * 40000).  N must be a multiple of 16.  Deterministic in `seed`. */
-int vd_synth_device(int options, size_t N, float snr, uint64_t seed, void* bits_d, void* packed_d,
-                    void* stream);
+/* ---- the reference harness's channel source (RandBitGen | ConvolutionalEncoder | AddNoise |
+ *      SoftDecisionPacker, viterbiDF.h:20-167), host and GPU ---- */
 
 /* Host-side reference-harness generator (std::mt19937 bits + std::normal_distribution<float>
  * noise, exactly the reference pipeline's semantics, viterbiDF.h:20-167, main.cpp:131-137). */
@@ -145,9 +137,10 @@ int vd_mt_state_after(uint32_t seed, uint64_t n, uint32_t* state624);
 long long vd_count_errors(int options, const uint8_t* bits, size_t N, const void* decoded, size_t decodedBytes);
 
 /* ---- runtime info ---- */
-/* split launches (DESIGN.md §4 "load balance"): how many split chunks were re-decoded whole on a device
- * because a speculative piece start did not converge (all launches so far; decoded words are exact
- * either way).  Set VD_NO_SPLIT=1 in the environment to disable splitting. */
+/* split launches (DESIGN.md §4 "load balance"): how many pieces of split chunks were re-decoded on a
+ * device because their speculative start had not converged at the piece boundary (all launches so far;
+ * decoded words are exact either way).  VD_NO_SPLIT=1 in the environment (read once per process and
+ * device) disables splitting. */
 int vd_split_redecodes(int device, uint64_t* count);
 const char* vd_last_error(void);
 int vd_device_count(void);

@@ -53,3 +53,44 @@ def test_no_gpu_exits_with_reference_convention():
         pytest.skip("GPU visible")
     r = run("-n", "2048", "--seed", "1,2")
     assert r.returncode == 1 and "vitdec create failed" in r.stderr
+
+
+PACK_PROBE = r"""
+#include <cstdio>
+#include "viterbiDF.h"
+int main(int argc, char** argv)
+{
+    const int ch = atoi(argv[1]);
+    Reals v;
+    float x;
+    while (scanf("%a", &x) == 1) v.push_back(x);
+    SoftDecisionPacker p((ChannelIn)ch, 1.0f);
+    const Soft out = std::any_cast<Soft>(p.process(OptData(std::any(v))));
+    for (soft_t w : out) printf("%u\n", (unsigned)w);
+    return 0;
+}
+"""
+
+
+@pytest.mark.parametrize("ch", [1, 2, 3])  # SOFT4, SOFT8, SOFT16
+def test_host_packer_matches_reference_quantiser_out_of_range(tmp_path, vo, ch):
+    """host/viterbiDF.h's SoftDecisionPacker quantises like the reference's (viterbiDF.h:106-125): for
+    SOFT4/SOFT8 lrintf's long is narrowed to int before saturating, for SOFT16 the long saturates, so
+    values with |v| >= 2^31 pack differently per format (checked against the oracle's vo_pack)."""
+    import numpy as np
+    src = tmp_path / "probe.cpp"
+    src.write_text(PACK_PROBE)
+    exe = tmp_path / "probe"
+    host = os.path.join(ROOT, "gpu-accelerated-viterbi-decoder_amd", "host")
+    subprocess.run(["g++", "-O1", "-std=c++17", "-I", host, "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)],
+                   check=True)
+    vals = np.array([2.0 ** 31, -2.0 ** 31, 2.0 ** 32 + 2 ** 9, -(2.0 ** 32) - 2 ** 9, 3.0e9, -3.0e9, 6.0e9, 1.0e12,
+                     -1.0e12, 127.5, -128.5, 7.49, -8.51, 32767.5, -32768.5, 0.5, -0.5, 1.5, 2.5, 1e-3],
+                     dtype=np.float32)
+    per = {1: 8, 2: 4, 3: 2}[ch]
+    vals = np.concatenate([vals, np.zeros((-len(vals)) % per, np.float32)])
+    r = subprocess.run([str(exe), str(ch)], input="\n".join(float(v).hex() for v in vals), capture_output=True,
+                       text=True, check=True)
+    host_words = np.array([int(x) for x in r.stdout.split()], dtype=np.uint32)
+    ref = vo.pack(ch, vals, scale=1.0).view(np.uint32)
+    assert np.array_equal(host_words, ref)

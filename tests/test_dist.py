@@ -45,7 +45,11 @@ def _worker(rank, world, port, q):
     seeds = [bench.rank_seed(rank, wi) for wi in range(2)]
     # the final gather of decoded words (uint8 buffers, as the decode writes them) to rank 0
     outs = _outs(rank)
-    _, gs = bench.gather_outputs(outs, "cpu", world, rank)
+    _, gs, err = bench.gather_outputs(outs, "cpu", world, rank)
+    assert err is None
+    # one rank cannot build its buffers (torch.cat of nothing raises): both ranks skip the collective
+    _, gs2, err2 = bench.gather_outputs(outs if rank == 0 else [], "cpu", world, rank)
+    assert gs2 is None and err2
     q.put((rank, m, g, seeds, gs))
     dist.barrier()
     dist.destroy_process_group()
@@ -81,3 +85,32 @@ def test_aggregate_is_whole_job():
     # 2 ranks x 2 batches x 31,999,936 bits in 1 step of 1 ms -> 256 Gb/s whole-job
     assert bench.aggregate_gbps(2 * 31_999_936, 2, 1, 1e-3) == pytest.approx(127.999744)
     assert bench.stages_per_launch(0x0, 64_000_000) == 1598 * 5088 + 4802 * 5056
+
+
+def _bench(*args, env=None):
+    import subprocess
+    e = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        e.pop(k, None)
+    e.update(env or {})
+    return subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *args], capture_output=True, text=True,
+                          timeout=180, env=e)
+
+
+def test_gpus_flag_launches_one_rank_per_gpu():
+    """`bench.py --gpus 2` (the driver's form) starts 2 ranks itself when no launcher set WORLD_SIZE
+    (here over gloo with --ranks-check, which touches no GPU)."""
+    import json
+    r = _bench("--gpus", "2", "--ranks-check")
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = json.loads(r.stdout.strip().splitlines()[-1])
+    assert line["n_gpus"] == 2
+    assert sorted(x["rank"] for x in line["ranks"]) == [0, 1]
+    assert sorted(x["local_rank"] for x in line["ranks"]) == [0, 1]
+
+
+def test_gpus_flag_must_match_launcher_world():
+    r = _bench("--gpus", "4", "--ranks-check", env={"WORLD_SIZE": "2", "RANK": "0", "LOCAL_RANK": "0"})
+    assert r.returncode != 0 and "--gpus 4 but WORLD_SIZE=2" in r.stderr
+    r = _bench("--gpus", "0", "--ranks-check")
+    assert r.returncode != 0

@@ -39,16 +39,22 @@ def test_cli_default_snr_is_error_free(gpu):
 
 
 @pytest.mark.gpu
-def test_run_batches_matches_single_runs(gpu, vo):
+@pytest.mark.parametrize("layout", ["every_device", "two_decoders_per_device"])
+def test_run_batches_matches_single_runs(gpu, vo, layout):
     # independent batches through vd_run_batches (the in-process multi-device API) are bit-exact
-    # against the oracle batch by batch
+    # against the oracle batch by batch: one decoder (thread) per visible device, and two
+    # decoders per device decoding concurrently (split launches of 16M-bit batches in flight together)
     opt = gpu.SOFT8 | gpu.M_B16
+    nbits = 400_000 if layout == "every_device" else 16_000_000
+    devices = list(range(gpu.device_count()))
+    if layout == "two_decoders_per_device":
+        devices = [d for d in devices for _ in range(2)]
     ins, refs = [], []
-    for i in range(3):
-        _, packed = vo.simulate(opt, 400_000, 1.0, 31 + i, 41 + i)
+    for i in range(max(3, len(devices) + 1)):
+        _, packed = vo.simulate(opt, nbits, 1.0, 31 + i, 41 + i)
         ins.append(packed)
-        refs.append(vo.decode(opt, packed)[0])
-    outs, ms = gpu.run_batches(opt, ins, 800_000, [0] * gpu.device_count())
+        refs.append(vo.decode(opt, packed, nthreads=16)[0])
+    outs, ms = gpu.run_batches(opt, ins, 2 * nbits, devices)
     assert ms > 0
     for o, r in zip(outs, refs):
         np.testing.assert_array_equal(o, r)

@@ -1,8 +1,9 @@
 """Split launches (vd_kernel_tg.h "split chunks"): with 6400 chunks on 1024 SIMDs the
 last 256 chunks are decoded as 4 pieces each, pieces 1-3 from a speculative start that is checked at
-the piece boundary; a failed check re-decodes the chunk whole.  The decoded words must be identical to
-the unsplit launch (VD_NO_SPLIT=1) and to the oracle, at SNRs where the speculation always converges
-and where it sometimes does not (SNR 0: the re-decode path runs)."""
+the piece boundary after a workgroup barrier; a piece whose check fails re-decodes from its left
+neighbour's end vector.  The decoded words must be identical to the unsplit launch (VD_NO_SPLIT=1) and
+to the oracle, at SNRs where the speculation always converges and where it often does not (SNR 0: the
+re-decode passes run, and the test requires that they did)."""
 import os
 
 import numpy as np
@@ -27,12 +28,18 @@ def decode_split_and_whole(gpu, opt, packed, n):
 @pytest.mark.gpu
 @pytest.mark.parametrize("opt", [HARD | M_B32, SOFT8 | M_B16, SOFT4 | M_B32, FP32 | M_FP16], ids=name)
 @pytest.mark.parametrize("snr", [0.0, 1.0, 3.0])
-def test_split_equals_whole_16m(gpu, opt, snr):
+def test_split_equals_whole_16m(gpu, vo, opt, snr):
     n = 16_000_000  # 78 words per chunk: split (>= 64)
     bits, packed = gpu_sim(gpu, opt, n, snr)
     out, whole, redecodes = decode_split_and_whole(gpu, opt, packed, n)
     bad = np.flatnonzero(out != whole)
-    assert bad.size == 0, f"{bad.size} words differ (re-decoded chunks: {redecodes}), first {bad[:5]}"
+    assert bad.size == 0, f"{bad.size} words differ (re-decoded pieces: {redecodes}), first {bad[:5]}"
+    ref, ok = vo.decode(opt, packed, nthreads=16)
+    assert ok
+    bad = np.flatnonzero(out != ref)
+    assert bad.size == 0, f"{bad.size} words differ from the oracle (re-decoded pieces: {redecodes}), first {bad[:5]}"
+    if snr == 0.0:  # at 0 dB speculative starts often have not converged: the re-decode passes ran
+        assert redecodes > 0
 
 
 def gpu_sim(gpu, opt, n, snr):
@@ -49,8 +56,8 @@ def gpu_sim(gpu, opt, n, snr):
 @pytest.mark.gpu
 @pytest.mark.slow
 @pytest.mark.parametrize("snr", [0.0, 1.2])
-def test_split_full_32m_matches_oracle(gpu, vo, snr):
-    opt = HARD | M_B32
+@pytest.mark.parametrize("opt", [HARD | M_B32, SOFT8 | M_B16], ids=name)
+def test_split_full_32m_matches_oracle(gpu, vo, opt, snr):
     bits, packed = gpu_sim(gpu, opt, 32_000_000, snr)
     before = gpu.split_redecodes()
     out = gpu_decode(gpu, opt, packed)
@@ -58,9 +65,9 @@ def test_split_full_32m_matches_oracle(gpu, vo, snr):
     ref, ok = vo.decode(opt, packed, nthreads=16)
     assert ok
     np.testing.assert_array_equal(out, ref)
-    print(f"snr {snr}: {redecodes} of 256 split chunks re-decoded")
+    print(f"snr {snr}: {redecodes} pieces of the 256 split chunks re-decoded")
     if snr == 0.0:
-        assert redecodes >= 0
+        assert redecodes > 0
 
 
 @pytest.mark.gpu

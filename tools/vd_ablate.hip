@@ -8,6 +8,7 @@
 #include <algorithm>
 #include "../gpu-accelerated-viterbi-decoder_amd/csrc/vd_kernels.h"
 #include "../gpu-accelerated-viterbi-decoder_amd/csrc/vd_kernel_tg.h"
+#include "vd_pk_kernel.h"
 
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP error %s at %d\n", hipGetErrorString(e), __LINE__); exit(1); } } while (0)
 
@@ -36,8 +37,8 @@ int main(int argc, char** argv)
     g.packNum = (N - 64) / 32;
     g.nchunks = 6400;
     g.availStages = N;
-    CK(hipMalloc(&g.fair, vd::kFairSlots * 8));
-    CK(hipMemset(g.fair, 0, vd::kFairSlots * 8));
+    CK(hipMalloc(&g.fair, vd::kFairBoardWords * 4));
+    CK(hipMemset(g.fair, 0xFF, vd::kFairBoardWords * 4));
     std::vector<Var> v;
     addb<0>(v, "sc hard/b32 full"); addb<1>(v, "sc hard/b32 -traceback");
     adds<0>(v, "sc soft8/b16 full");
@@ -47,6 +48,7 @@ int main(int argc, char** argv)
     tgs<0>(v, "tg soft8/b16 full"); tgs<1>(v, "tg soft8/b16 -traceback"); tgs<2>(v, "tg soft8/b16 -tabreads"); tgs<4>(v, "tg soft8/b16 -readout"); tgf<0>(v, "tg fp32/f16 full");
     tgb<262144>(v, "tg hard/b32 sub+add+maxdpp"); tgs<262144>(v, "tg soft8/b16 sub+add+maxdpp");
     tgb<524288>(v, "tg hard/b32 pkfma+maxdpp"); tgs<524288>(v, "tg soft8/b16 pkfma+maxdpp");
+    tgb<(1 << 20)>(v, "tg hard/b32 board sc1 loads"); tgs<(1 << 20)>(v, "tg soft8/b16 board sc1 loads");
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
     const int rounds = argc > 1 ? atoi(argv[1]) : 10;
@@ -95,10 +97,10 @@ int main(int argc, char** argv)
         }
         std::vector<int> hist(16, 0); int used = 0;
         for (int c : cnt) if (c) { used++; hist[std::min(c, 15)]++; }
-        std::vector<unsigned long long> fb(vd::kFairSlots);
-        CK(hipMemcpy(fb.data(), g.fair, fb.size() * 8, hipMemcpyDeviceToHost));
-        int nz = 0; for (auto x : fb) nz += x != 0;
-        printf("progress board words non-zero after run: %d\n", nz);
+        std::vector<uint32_t> fb(vd::kFairBoardWords);
+        CK(hipMemcpy(fb.data(), g.fair, fb.size() * 4, hipMemcpyDeviceToHost));
+        int nz = 0; for (auto x : fb) nz += x != vd::kFairEmpty;
+        printf("progress board slots still taken after run: %d\n", nz);
         printf("SIMDs used %d; waves-per-SIMD histogram:", used);
         for (int i = 0; i < 16; i++) if (hist[i]) printf(" %d:%d", i, hist[i]);
         printf("\n");

@@ -24,8 +24,8 @@ int main(int argc, char** argv)
     g.packNum = (N - 64) / 32;
     g.nchunks = 6400;
     g.availStages = N;
-    CK(hipMalloc(&g.fair, vd::kFairSlots * 8));
-    CK(hipMemset(g.fair, 0, vd::kFairSlots * 8));
+    CK(hipMalloc(&g.fair, vd::kFairBoardWords * 4));
+    CK(hipMemset(g.fair, 0xFF, vd::kFairBoardWords * 4));
     std::vector<Var> v = {
         {"new hard/b32", (KFn)vd::vd_decode_tg<vd::HARD, vd::B32, 32, 0>}, {"old hard/b32", (KFn)vd::old::vd_decode_tg<vd::HARD, vd::B32, 32, 0>},
         {"new soft8/b16", (KFn)vd::vd_decode_tg<vd::SOFT8, vd::B16, 32, 0>}, {"old soft8/b16", (KFn)vd::old::vd_decode_tg<vd::SOFT8, vd::B16, 32, 0>},

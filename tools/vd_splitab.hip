@@ -36,16 +36,15 @@ int main(int argc, char** argv)
     g.nchunks = 6400;
     g.availStages = N;
     g.scale = 1.0f;
-    CK(hipMalloc(&g.fair, vd::kFairSlots * 8));
-    CK(hipMemset(g.fair, 0, vd::kFairSlots * 8));
-    float* spec; uint32_t* flags;
-    CK(hipMalloc(&spec, 256 * 4 * 64 * 4));
-    CK(hipMalloc(&flags, (256 * 16 + 1) * 4));
-    CK(hipMemset(flags, 0, (256 * 16 + 1) * 4));
-    uint32_t epoch = 0;
+    CK(hipMalloc(&g.fair, vd::kFairBoardWords * 4));
+    CK(hipMemset(g.fair, 0xFF, vd::kFairBoardWords * 4));
+    float* spec; uint32_t* stats;
+    CK(hipMalloc(&spec, 256 * vd::kSplitVecs * 64 * 4));
+    CK(hipMalloc(&stats, 4));
+    CK(hipMemset(stats, 0, 4));
     auto launch = [&](KFn f, bool split) {
         vd::Geom q = g;
-        if (split) { q.nwhole = 6144; q.epoch = ++epoch; q.spec = spec; q.flags = flags; q.stats = flags + 256 * 16; }
+        if (split) { q.nwhole = 6144; q.spec = spec; q.stats = stats; }
         hipLaunchKernelGGL(f, dim3(split ? 1792 : 1600), dim3(256), 0, 0, in, out, q);
     };
     KFn f0 = (KFn)vd::vd_decode_tg<vd::HARD, vd::B32, 32, 0>, f32 = (KFn)vd::vd_decode_tg<vd::HARD, vd::B32, 32, 32>;
@@ -60,7 +59,7 @@ int main(int argc, char** argv)
         }
     for (int s = 0; s < 2; s++) { std::sort(t[s].begin(), t[s].end());
         printf("%-8s median %.4f ms  min %.4f ms\n", s ? "split" : "plain", t[s][t[s].size() / 2], t[s][0]); }
-    uint32_t redec = 0; CK(hipMemcpy(&redec, flags + 256 * 16, 4, hipMemcpyDeviceToHost));
+    uint32_t redec = 0; CK(hipMemcpy(&redec, stats, 4, hipMemcpyDeviceToHost));
     printf("re-decoded split chunks over all split launches: %u\n", redec);
     for (int s = 0; s < 2; s++) {
         const int nw = s ? 7168 : 6400;

@@ -25,8 +25,8 @@ int main(int argc, char** argv)
     g.nchunks = 6400;
     g.availStages = N;
     g.scale = 1.0f;
-    CK(hipMalloc(&g.fair, vd::kFairSlots * 8));
-    CK(hipMemset(g.fair, 0, vd::kFairSlots * 8));
+    CK(hipMalloc(&g.fair, vd::kFairBoardWords * 4));
+    CK(hipMemset(g.fair, 0xFF, vd::kFairBoardWords * 4));
     std::vector<Var> v = {hb<0>("full (xor16 swizzle q4)"), hb<131072>("map B: swizzle q2, permlane q5"),
                           hb<131072 | 8192>("map B: swizzle q2, bpermute q5"), hb<8192>("map A: swizzle q4, bpermute q5"),
                           hb<128>("all-dpp"), hb<1 | 2 | 4 | 8 | 16>("ACS only"), hb<1 | 2 | 4 | 8 | 16 | 131072 | 8192>("ACS only, map B both LDS"),

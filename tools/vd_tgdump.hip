@@ -20,7 +20,7 @@ int main(int argc, char** argv)
     g.nchunks = argc > 3 ? atoi(argv[3]) : 1;
     g.fair = nullptr;
     const int fair = argc > 4 ? atoi(argv[4]) : 0;
-    if (fair) { CK(hipMalloc(&g.fair, vd::kFairSlots * 8)); CK(hipMemset(g.fair, 0, vd::kFairSlots * 8)); }
+    if (fair) { CK(hipMalloc(&g.fair, vd::kFairBoardWords * 4)); CK(hipMemset(g.fair, 0xFF, vd::kFairBoardWords * 4)); }
     void *din, *dout;
     CK(hipMalloc(&din, nw * 4));
     CK(hipMalloc(&dout, (8u << 20)));
