@@ -99,12 +99,17 @@ static_assert(tg_label(32, 0) == 0 && tg_label(16, 5) == 0, "swap partners share
 // name the pair v[60:61] and read V for both of its halves (op_sel_hi 0); v62:v63 are its scratch.
 typedef float f2v __attribute__((ext_vector_type(2)));
 // DPP stage, exchange lane xor {1,2,7,8}[Q].  The DPP source (V) is >= 2 VALU slots after its write.
-template <int Q>
+template <int Q, bool NOP = true>
 __device__ __forceinline__ void tg_stage_dpp(float& V, float m)
 {
     float t1, t2;
 #define VD_TG_DPP(CTRL)                                                                                   \
+    if constexpr (NOP)                                                                                    \
     asm("v_add_f32 %1, %0, %3\n\ts_nop 0\n\tv_sub_f32_dpp %2, %0, %3 " CTRL " row_mask:0xf bank_mask:0xf\n\t" \
+        "v_max_f32 %0, %1, %2"                                                                           \
+        : "+{v60}"(V), "=&v"(t1), "=&v"(t2) : "v"(m));                                                   \
+    else                                                                                                  \
+    asm("v_add_f32 %1, %0, %3\n\tv_sub_f32_dpp %2, %0, %3 " CTRL " row_mask:0xf bank_mask:0xf\n\t"      \
         "v_max_f32 %0, %1, %2"                                                                           \
         : "+{v60}"(V), "=&v"(t1), "=&v"(t2) : "v"(m))
     if constexpr (Q == 0) VD_TG_DPP("quad_perm:[1,0,3,2]");
@@ -359,14 +364,26 @@ template <> struct TgIn<kLlr + HARD> : TgInLlr<HARD> {};
 template <> struct TgIn<kLlr + SOFT4> : TgInLlr<SOFT4> {};
 template <> struct TgIn<kLlr + SOFT8> : TgInLlr<SOFT8> {};
 template <> struct TgIn<kLlr + FP32> : TgInLlr<FP32> {};
-// resource for the 96 stages from g0 (g0 a multiple of 16; inputs below 4 GiB)
+// resource for the 96 stages from g0 (g0 a multiple of 16).
+// The range min(max(availBytes - off, 0), 2^32 - 1) is computed on the scalar unit with 32-bit halves
+// (SCC carries the borrow): gfx950 has no scalar 64-bit compare, and hipcc's vector compare plus its
+// VCC -> scalar select stalled every group head.
 template <int CH>
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t tg_rsrc(const void* in, uint64_t g0, uint64_t availBytes)
 {
     const uint64_t off = TgIn<CH>::bytes(g0);
-    const uint64_t rem = availBytes > off ? availBytes - off : 0;
-    return __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)in + off), (short)0,
-                                             (int)(uint32_t)(rem < 0xFFFFFFFFull ? rem : 0xFFFFFFFFull), 0x00020000);
+    uint32_t lo, hi;
+    asm("s_sub_u32 %[lo], %[al], %[ol]\n\t"
+        "s_subb_u32 %[hi], %[ah], %[oh]\n\t"  // SCC = borrow: the group starts past the data
+        "s_cselect_b32 %[lo], 0, %[lo]\n\t"
+        "s_cselect_b32 %[hi], 0, %[hi]\n\t"
+        "s_cmp_lg_u32 %[hi], 0\n\t"
+        "s_cselect_b32 %[lo], -1, %[lo]"
+        : [lo] "=&s"(lo), [hi] "=&s"(hi)
+        : [al] "s"((uint32_t)availBytes), [ah] "s"((uint32_t)(availBytes >> 32)), [ol] "s"((uint32_t)off),
+          [oh] "s"((uint32_t)(off >> 32))
+        : "scc");
+    return __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)in + off), (short)0, (int)lo, 0x00020000);
 }
 
 // ---------------------------------------------------------------- split chunks
@@ -564,7 +581,9 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(7))
                 tg_stage_dpp2<DCTRL, ODD ? 1 : 0, (ABL & 524288) != 0>(V, e, spm);
             } else if constexpr ((!IS16 && !IS32) || (ABL & 128)) {
                 const float m = (ABL & 2) ? (float)aK[K] : (ODD ? vp[RP].y : vp[RP].x);
-                tg_stage_dpp<DCTRL>(V, m);
+                // ABL 1<<21 (study): no s_nop inside the stage where hipcc pads the asm boundary itself
+                constexpr bool NOPD = !(ABL & (1 << 21)) || i % 16 == 0;
+                tg_stage_dpp<DCTRL, NOPD>(V, m);
             } else if constexpr (LSW) {
                 const float pv = IS16 ? __builtin_bit_cast(float, __builtin_amdgcn_ds_swizzle(__builtin_bit_cast(int, V), 0x401F))
                                       : tg_partner(V, pa5);
@@ -576,18 +595,32 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(7))
             }
             if constexpr (r + TGD < 96) issue(std::integral_constant<int, r + TGD>{});
             if constexpr (i % J == J - 1 && !(ABL & 4)) {
-                // field read-out: bits (2^(S-1) + h) >> 1 = (h + 2^J - 1) / 2, then clear to 2^(S-1)
-                uint32_t bits;
-                asm("v_bfe_u32 %1, %0, 1, %4\n\tv_and_or_b32 %0, %0, %2, %3"
-                    : "+{v60}"(V), "=&v"(bits) : "v"(fnm), "v"(fhf), "n"(J));
+                // field read-out: bits 1..J of the pattern, (2^(S-1) + h) >> 1 = (h + 2^J - 1) / 2, go straight
+                // into byte / half g of the block's ring word (SDWA dst_sel: one op for shift and merge), then
+                // the field is cleared to 2^(S-1).  Every 16 stages the decision-neutral renormalisation by
+                // the metric of position 0 follows: readfirstlane (1 wait state after the clear), the
+                // offset on the scalar unit, one vector subtract.
                 constexpr int g = (i % 32) / J;
-                if constexpr (g == 0) word = bits;
-                else word |= bits << (J * g);
-                if constexpr (i % 16 == 15) {
-                    // decision-neutral renormalisation by the metric of position 0, every 16 stages
-                    const uint32_t p0 = __builtin_amdgcn_readfirstlane(__builtin_bit_cast(uint32_t, V));
-                    V = __builtin_bit_cast(float, __builtin_bit_cast(uint32_t, V) - (p0 - VBASE));
-                }
+                uint32_t sr;
+#define VD_TG_RO(SEL, UNUSED) "v_lshrrev_b32_sdwa %[w], 1, %[V] dst_sel:" SEL " dst_unused:" UNUSED             \
+                              " src0_sel:DWORD src1_sel:DWORD\n\tv_and_or_b32 %[V], %[V], %[fnm], %[fhf]"
+#define VD_TG_RN "\n\ts_nop 0\n\tv_readfirstlane_b32 %[sr], %[V]\n\ts_sub_u32 %[sr], %[sr], %[vb]\n\tv_subrev_u32 %[V], %[sr], %[V]"
+#define VD_TG_IN [fnm] "v"(fnm), [fhf] "v"(fhf), [vb] "n"(VBASE)
+                if constexpr (J == 8 && g == 0)
+                    asm(VD_TG_RO("BYTE_0", "UNUSED_PAD") : [V] "+{v60}"(V), [w] "=&v"(word) : VD_TG_IN);
+                else if constexpr (J == 8 && g == 1)
+                    asm(VD_TG_RO("BYTE_1", "UNUSED_PRESERVE") VD_TG_RN : [V] "+{v60}"(V), [w] "+v"(word), [sr] "=&s"(sr) : VD_TG_IN);
+                else if constexpr (J == 8 && g == 2)
+                    asm(VD_TG_RO("BYTE_2", "UNUSED_PRESERVE") : [V] "+{v60}"(V), [w] "+v"(word) : VD_TG_IN);
+                else if constexpr (J == 8)
+                    asm(VD_TG_RO("BYTE_3", "UNUSED_PRESERVE") VD_TG_RN : [V] "+{v60}"(V), [w] "+v"(word), [sr] "=&s"(sr) : VD_TG_IN);
+                else if constexpr (g == 0)
+                    asm(VD_TG_RO("WORD_0", "UNUSED_PAD") VD_TG_RN : [V] "+{v60}"(V), [w] "=&v"(word), [sr] "=&s"(sr) : VD_TG_IN);
+                else
+                    asm(VD_TG_RO("WORD_1", "UNUSED_PRESERVE") VD_TG_RN : [V] "+{v60}"(V), [w] "+v"(word), [sr] "=&s"(sr) : VD_TG_IN);
+#undef VD_TG_IN
+#undef VD_TG_RN
+#undef VD_TG_RO
             }
         });
         // ring word of position p: byte (J=8) / half (J=16) g = the J path bits of the survivor that

@@ -411,11 +411,12 @@ struct Fair {
             x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xF, 0xF, true);
             x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xF, 0xF, true);
             const uint32_t sum = (uint32_t)__builtin_amdgcn_readlane((int)x, 15);
-            // (own - mean) * n in blocks; own word read back as posted at the previous head (j - 3)
-            const int64_t d = (int64_t)(j - 3) * n - (int64_t)sum;
-            if (d <= -3 * (int64_t)n) __builtin_amdgcn_s_setprio(3);
+            // (own - mean) * n in blocks; own word read back as posted at the previous head (j - 3).
+            // 32-bit scalar arithmetic (n <= 16, j < 2^26): 64-bit compares would run on the VALU.
+            const int32_t d = (int32_t)(j - 3) * (int32_t)n - (int32_t)sum, n3 = 3 * (int32_t)n;
+            if (d <= -n3) __builtin_amdgcn_s_setprio(3);
             else if (d <= 0) __builtin_amdgcn_s_setprio(2);
-            else if (d <= 3 * (int64_t)n) __builtin_amdgcn_s_setprio(1);
+            else if (d <= n3) __builtin_amdgcn_s_setprio(1);
             else __builtin_amdgcn_s_setprio(0);
         }
         if (lane == 0) __hip_atomic_store(mine, j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);

@@ -1,5 +1,8 @@
+# ablation / exact-twin timing run: gpurun -- bash scripts/gpu_abl.sh <tag> [rounds]
 set -o pipefail
 cd $GRAFT_REPO_ROOT
-timeout -k 10 120 tools/vd_ablate ${1:-8} > gpurun_out/ablate.log 2>&1
-echo abl_rc=$?
-cat gpurun_out/ablate.log
+O=gpurun_out/${1:-abl}
+mkdir -p $O
+timeout -k 10 300 tools/vd_ablate ${2:-5} > $O/ablate.log 2>&1
+echo rc=$?
+grep -v "^===\|kernel span\|wave \|clock\|cycles/stage\|progress\|SIMDs" $O/ablate.log

@@ -6,6 +6,7 @@
 #include <cstdlib>
 #include <vector>
 #include <algorithm>
+#include <cstring>
 #include "../gpu-accelerated-viterbi-decoder_amd/csrc/vd_kernels.h"
 #include "../gpu-accelerated-viterbi-decoder_amd/csrc/vd_kernel_tg.h"
 #include "vd_pk_kernel.h"
@@ -13,7 +14,7 @@
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP error %s at %d\n", hipGetErrorString(e), __LINE__); exit(1); } } while (0)
 
 using KFn = void (*)(const void*, void*, vd::Geom);
-struct Var { const char* name; KFn fn; int grid; int block = 256; };
+struct Var { const char* name; KFn fn; int grid; int block = 256; int ref = -1; };  // ref: exact twin
 
 template <int ABL> void addb(std::vector<Var>& v, const char* n) { v.push_back({n, (KFn)vd::vd_decode_sc<vd::HARD, vd::B32, 32, ABL>, 1600}); }
 template <int ABL> void adds(std::vector<Var>& v, const char* n) { v.push_back({n, (KFn)vd::vd_decode_sc<vd::SOFT8, vd::B16, 32, ABL>, 1600}); }
@@ -49,6 +50,18 @@ int main(int argc, char** argv)
     tgb<262144>(v, "tg hard/b32 sub+add+maxdpp"); tgs<262144>(v, "tg soft8/b16 sub+add+maxdpp");
     tgb<524288>(v, "tg hard/b32 pkfma+maxdpp"); tgs<524288>(v, "tg soft8/b16 pkfma+maxdpp");
     tgb<(1 << 20)>(v, "tg hard/b32 board sc1 loads"); tgs<(1 << 20)>(v, "tg soft8/b16 board sc1 loads");
+    tgb<(1 << 21)>(v, "tg hard/b32 dpp no inner nop"); tgs<(1 << 21)>(v, "tg soft8/b16 dpp no inner nop");
+    // variants that must decode exactly like the full kernel: outputs compared word for word below
+    auto twin = [&](const char* a, const char* b) {
+        int ia = -1, ib = -1;
+        for (size_t i = 0; i < v.size(); i++) { if (!strcmp(v[i].name, a)) ia = (int)i; if (!strcmp(v[i].name, b)) ib = (int)i; }
+        if (ia >= 0 && ib >= 0) v[ib].ref = ia;
+    };
+    for (const char* k : {"sub+add+maxdpp", "pkfma+maxdpp", "board sc1 loads", "dpp no inner nop"}) {
+        char a[96], b[96];
+        snprintf(a, sizeof a, "tg hard/b32 full"); snprintf(b, sizeof b, "tg hard/b32 %s", k); twin(a, b);
+        snprintf(a, sizeof a, "tg soft8/b16 full"); snprintf(b, sizeof b, "tg soft8/b16 %s", k); twin(a, b);
+    }
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
     const int rounds = argc > 1 ? atoi(argv[1]) : 10;
@@ -66,6 +79,24 @@ int main(int argc, char** argv)
         std::sort(t[i].begin(), t[i].end());
         printf("%-26s median %.4f ms  min %.4f ms  -> %.1f Gb/s\n", v[i].name, t[i][t[i].size() / 2], t[i][0],
                (double)(N - 64) / (t[i][t[i].size() / 2] * 1e-3) / 1e9);
+    }
+    // exact twins: the same decoded words as the full kernel
+    {
+        const size_t nb = g.packNum * 4;
+        std::vector<uint32_t> a(nb / 4), b(nb / 4);
+        for (size_t i = 0; i < v.size(); i++) {
+            if (v[i].ref < 0) continue;
+            const Var& r = v[v[i].ref];
+            CK(hipMemset(out, 0, nb));
+            hipLaunchKernelGGL(r.fn, dim3(r.grid), dim3(r.block), 0, 0, in, out, g);
+            CK(hipMemcpy(a.data(), out, nb, hipMemcpyDeviceToHost));
+            CK(hipMemset(out, 0, nb));
+            hipLaunchKernelGGL(v[i].fn, dim3(v[i].grid), dim3(v[i].block), 0, 0, in, out, g);
+            CK(hipMemcpy(b.data(), out, nb, hipMemcpyDeviceToHost));
+            size_t bad = 0;
+            for (size_t k = 0; k < a.size(); k++) bad += a[k] != b[k];
+            printf("exact twin %-30s vs %-22s: %zu of %zu words differ\n", v[i].name, r.name, bad, a.size());
+        }
     }
     // per-wave clock stamps of the full kernel (ABL 32), without and with the priority schedule (64)
     for (KFn f : {(KFn)vd::vd_decode_sc<vd::HARD, vd::B32, 32, 32>, (KFn)vd::vd_decode_tg<vd::HARD, vd::B32, 32, 32>}) {
