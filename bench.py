@@ -30,7 +30,7 @@ import vitdec  # noqa: E402
 N_BITS = 32_000_000
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md)
 SNR_DB = 2.0
-PMC_ROUND = "r01"  # profiles/<round>/pmc_summary.json
+PMC_ROUND = "r02"  # profiles/<round>/pmc_summary.json, profiles/<round>/ablate.log
 
 WORKLOADS = [
     ("hard_b32", vitdec.HARD | vitdec.M_B32 | vitdec.O_B32),
@@ -106,8 +106,57 @@ def load_pmc():
     return {}
 
 
-CLOCK_HZ = 2.4e9  # gfx950 peak engine clock (MI355X_MICROARCH.md)
 N_SIMD = 1024     # 256 CUs x 4 SIMDs
+N_XCD = 8         # rocprofv3 sums GRBM_GUI_ACTIVE over the 8 XCDs (MI355X_MICROARCH.md, DVFS give-back)
+
+
+def acs_only_ms(name):
+    """Instruction-mix ceiling of a workload's kernel: the time of the same launch with only the ACS
+    recursion left (tools/vd_ablate 'ACS only' variant: no table build/reads, read-out, loads or
+    traceback), from the committed ablation log of this round; None if absent."""
+    key = {"hard_b32": "tg hard/b32 ACS only ", "soft8_b16": "tg soft8/b16 ACS only "}.get(name)
+    p = os.path.join(ROOT, "profiles", PMC_ROUND, "ablate.log")
+    if key is None or not os.path.exists(p):
+        return None
+    with open(p) as f:
+        for line in f:
+            if line.startswith(key) and "median" in line:
+                return float(line.split("median")[1].split()[0])
+    return None
+
+
+def valu_view(pmc, kernel_ms, stages, name, msg_bits):
+    """The bound that binds: VALU issue.  From the committed PMC summary of this kernel
+    (counters per dispatch, summed over the chip) and the live kernel time:
+      clock        = GRBM_GUI_ACTIVE / 8 XCDs / kernel time            (measured engine clock)
+      busy_pct     = 100 * SQ_ACTIVE_INST_VALU * 4 / (1024 SIMDs * GRBM_GUI_ACTIVE / 8)
+                     (the gfx94x VALUBusy formula rocprofv3 falls back to on gfx950; it charges 4 cycles
+                     per wave64 VALU instruction, a SIMD-16 model, so it reads above 100 on the 32-lane
+                     gfx950 SIMD when every SIMD issues VALU back to back)
+      issue_pct    = 100 * SQ_INSTS_VALU * 2 / (1024 * GRBM_GUI_ACTIVE / 8)
+                     (SIMD-32 model: a wave64 VALU instruction occupies its SIMD for 2 cycles at the
+                     least; max/DPP/permlane/bit-field forms take 4 -- profiles/r01/ubench_maxcost.log)
+      mix ceiling  = the same launch with only the ACS recursion (tools/vd_ablate)."""
+    c = pmc.get("counters_mean_per_dispatch", {})
+    if not c or "SQ_INSTS_VALU" not in c:
+        return None
+    insts = c["SQ_INSTS_VALU"]
+    v = {"insts_per_launch": round(insts), "insts_per_wave_stage": round(insts / stages, 3),
+         "wave_stages_per_launch": stages}
+    if "GRBM_GUI_ACTIVE" in c:
+        cyc = c["GRBM_GUI_ACTIVE"] / N_XCD
+        v["clock_ghz"] = round(cyc / (kernel_ms * 1e-3) / 1e9, 3)
+        v["issue_pct"] = round(100.0 * insts * 2 / (N_SIMD * cyc), 1)
+        if "SQ_ACTIVE_INST_VALU" in c:
+            v["busy_pct"] = round(100.0 * c["SQ_ACTIVE_INST_VALU"] * 4 / (N_SIMD * cyc), 1)
+        v["cycles_per_inst_per_simd"] = round(N_SIMD * cyc / insts, 3)
+    acs = acs_only_ms(name)
+    if acs:
+        v["mix_ceiling"] = {"acs_only_ms": acs, "gbps": round(msg_bits / (acs * 1e-3) / 1e9, 2),
+                            "frac": round(acs / kernel_ms, 3),
+                            "source": f"profiles/{PMC_ROUND}/ablate.log (random input, unsplit launch)"}
+    v["source"] = f"profiles/{PMC_ROUND}/pmc_summary.json"
+    return v
 
 
 def stages_per_launch(opt, input_num):
@@ -468,15 +517,9 @@ def main():
         achieved = alg / (kms[di] * 1e-3) / 1e9
         pmc = load_pmc().get(db["name"], {})
         traffic = pmc.get("traffic_bytes")
-        # VALU issue view of the same kernel (the bound that actually binds)
+        # VALU view of the same kernel (the bound that binds)
         stages = stages_per_launch(db["opt"], db["input_num"])
-        valu = None
-        if "counters_mean_per_dispatch" in pmc and "SQ_INSTS_VALU" in pmc["counters_mean_per_dispatch"]:
-            insts = pmc["counters_mean_per_dispatch"]["SQ_INSTS_VALU"]  # all waves of the launch (split pieces too)
-            valu = {"insts_per_launch": round(insts), "insts_per_wave_stage": round(insts / stages, 3),
-                    "wave_stages_per_launch": stages,
-                    "issue_cycles_per_inst_per_simd": round(kms[di] * 1e-3 * CLOCK_HZ * N_SIMD / insts, 3),
-                    "source": f"profiles/{PMC_ROUND}/pmc_summary.json (SQ_INSTS_VALU)"}
+        valu = valu_view(pmc, kms[di], stages, db["name"], db["msg"])
         result = {
             "metric": "decoded Gb/s at K=7 R=1/2, 32M bits, hard+soft8",
             "value": round(value, 3),
@@ -505,7 +548,9 @@ def main():
                 "kernels": {b["name"]: vitdec.kernel_name(b["opt"]) for b in batches},
             },
             "roofline": {
-                "bound": "hbm",
+                "bound": "valu",
+                "bound_note": "VALU issue binds (add-compare-select, no MFMA); achieved/peak/frac are the HBM "
+                              "view north_star asks for, valu holds the binding view",
                 "kernel": db["name"] + ": " + vitdec.kernel_name(db["opt"]),
                 "achieved": round(achieved, 2),
                 "peak": HBM_PEAK_GBS,

@@ -104,15 +104,11 @@ unsigned tg_grid(const vd::Geom& g)
     return g.nwhole / vd::kWaves + (g.nchunks - g.nwhole);
 }
 
+// the tagged-metric kernel for every format (SOFT16 on int32 patterns, vd_kernel_tg.h TgFmt::INT)
 template <int CH, int CORE, int OB>
 void launch_t(const void* in, void* out, vd::Geom g, hipStream_t s)
 {
-    // tagged-metric kernel everywhere but SOFT16 (whose metrics leave no room for the tags)
-    if constexpr (CH == vd::SOFT16)
-        hipLaunchKernelGGL((vd::vd_decode_sc<CH, CORE, OB>), dim3((g.nchunks + vd::kWaves - 1) / vd::kWaves),
-                           dim3(64 * vd::kWaves), 0, s, in, out, g);
-    else
-        hipLaunchKernelGGL((vd::vd_decode_tg<CH, CORE, OB>), dim3(tg_grid(g)), dim3(64 * vd::kWaves), 0, s, in, out, g);
+    hipLaunchKernelGGL((vd::vd_decode_tg<CH, CORE, OB>), dim3(tg_grid(g)), dim3(64 * vd::kWaves), 0, s, in, out, g);
 }
 
 template <int CH, int CORE>
@@ -146,7 +142,6 @@ launch_fn pick_llr_ob(int ob)
 {
     return ob == 1 ? &launch_llr_t<CH, CORE, 16> : &launch_llr_t<CH, CORE, 32>;
 }
-// null for SOFT16 (its metrics need the untagged kernel: pack first, then decode)
 launch_fn pick_llr(int o)
 {
     const int ch = ch_of(o), me = met_of(o), ob = out_of(o);
@@ -154,6 +149,7 @@ launch_fn pick_llr(int o)
     case 0: return me == 0 ? pick_llr_ob<0, 0>(ob) : me == 1 ? pick_llr_ob<0, 1>(ob) : pick_llr_ob<0, 2>(ob);
     case 1: return me == 0 ? pick_llr_ob<1, 0>(ob) : me == 1 ? pick_llr_ob<1, 1>(ob) : pick_llr_ob<1, 2>(ob);
     case 2: return me == 0 ? pick_llr_ob<2, 0>(ob) : pick_llr_ob<2, 1>(ob);
+    case 3: return pick_llr_ob<3, 0>(ob);
     case 4: return me == 0 ? pick_llr_ob<4, 0>(ob) : me == 1 ? pick_llr_ob<4, 1>(ob) : pick_llr_ob<4, 2>(ob);
     }
     return nullptr;
@@ -165,7 +161,7 @@ const char* kname(int o)
         {"vd_decode_tg<HARD,B32>", "vd_decode_tg<HARD,B16>", "vd_decode_tg<HARD,F16>"},
         {"vd_decode_tg<SOFT4,B32>", "vd_decode_tg<SOFT4,B16>", "vd_decode_tg<SOFT4,F16>"},
         {"vd_decode_tg<SOFT8,B32>", "vd_decode_tg<SOFT8,B16>", "-"},
-        {"vd_decode_sc<SOFT16,B32>", "-", "-"},
+        {"vd_decode_tg<SOFT16,B32> (int32 patterns)", "-", "-"},
         {"vd_decode_tg<FP32,B32>", "vd_decode_tg<FP32,B16>", "vd_decode_tg<FP32,F16>"},
     };
     if (!valid(o)) return "-";
@@ -272,7 +268,7 @@ static DeviceState* device_state(int device)
 // on 1024 SIMDs: 6 whole chunks per SIMD + 256 chunks in 4 pieces) and the chunks are long enough
 static void plan_split(vd::Geom& g, int options, DeviceState* x)
 {
-    if (out_of(options) != 0 || ch_of(options) == vd::SOFT16) return;  // O_B32, tagged kernel only
+    if (out_of(options) != 0) return;  // O_B32 only
     const uint32_t perSimd = g.nchunks / (uint32_t)x->nsimd, rem = g.nchunks % (uint32_t)x->nsimd;
     if (rem == 0 || rem * vd::kWaves != (uint32_t)x->nsimd || perSimd + 1 > 7) return;
     if (g.packNum / g.nchunks < (uint64_t)vd::kSplitMinWords) return;
@@ -449,16 +445,7 @@ int vd_run_device_llr(vd_decoder* d, const float* llr_d, void* output_d, size_t 
 {
     if (!d || !llr_d || !output_d) return fail(VD_ERR_ARG, "null argument");
     if (message_len(d->options, inputNum) == 0) return fail(VD_ERR_ARG, "inputNum too small");
-    hipStream_t s = (hipStream_t)stream;
-    if (ch_of(d->options) == 3) {  // SOFT16: pack into the decoder's buffer, then the untagged decode
-        VD_HIP(hipSetDevice(d->device));
-        int rc = ensure_capacity(d, input_size(d->options, inputNum), 0);
-        if (rc != VD_OK) return rc;
-        rc = launch_pack(d->options, llr_d, inputNum, scale, d->in_d, s);
-        if (rc != VD_OK) return rc;
-        return launch_decode(d, d->in_d, output_d, inputNum, s);
-    }
-    return launch_decode(d, llr_d, output_d, inputNum, s, true, scale);
+    return launch_decode(d, llr_d, output_d, inputNum, (hipStream_t)stream, true, scale);
 }
 
 int vd_run_llr(vd_decoder* d, const float* llr_h, void* output_h, size_t inputNum, float scale, float* kernel_ms)
@@ -474,7 +461,7 @@ int vd_run_llr(vd_decoder* d, const float* llr_h, void* output_h, size_t inputNu
         VD_HIP(hipMalloc(&d->llr_d, inB));
         d->cap_llr = inB;
     }
-    int rc = ensure_capacity(d, ch_of(d->options) == 3 ? input_size(d->options, inputNum) : 0, outB + 16);
+    int rc = ensure_capacity(d, 0, outB + 16);
     if (rc != VD_OK) return rc;
     VD_HIP(hipMemcpyAsync(d->llr_d, llr_h, inB, hipMemcpyHostToDevice, d->stream));
     VD_HIP(hipEventRecord(d->ev0, d->stream));

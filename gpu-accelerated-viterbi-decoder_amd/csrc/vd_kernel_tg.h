@@ -17,6 +17,10 @@
 // (0, 2^S), its decision bits (h + 2^J - 1) / 2 are mantissa bits 1..J, and clearing it is one
 // v_and_or_b32.  Renormalising every 16 stages keeps |metric| < 2^(22-S).
 //
+// SOFT16 (|BM| up to 65536: a metric spread near 2^21) leaves no room for the tags below 2^24, so its
+// kernel runs the same scheme on int32 patterns (TgFmt::INT): V = metric * 2^S + 2^(S-1) + h with |V| <
+// 2^30, integer add / DPP subtract / signed max, and the same bit-field read-out.
+//
 // Lane encoding.  Position p (the trellis state rotr6(p, t%6) after stage t, as in vd_decode_sc) lives
 // in lane l = p0*1 ^ p1*2 ^ p2*7 ^ p3*8 ^ p4*16 ^ p5*32, so the butterfly partner p ^ (1<<q) is lane
 // l ^ {1, 2, 7, 8, 16, 32}[q]: DPP quad_perm (xor 1, 2), row_half_mirror (xor 7), row_ror:8 (xor 8)
@@ -34,13 +38,14 @@ namespace vd {
 constexpr int kLlr = 8;
 template <int CH>
 struct TgFmt {
-    static_assert((CH & 7) != SOFT16, "SOFT16 metrics do not leave room for decision tags");
+    static constexpr bool INT = (CH & 7) == SOFT16;      // int32 metric patterns instead of fp32
     static constexpr int J = (CH & 7) == HARD ? 16 : 8;  // stages per history field
-    static constexpr int S = J + 1;                // metric scale 2^S
+    static constexpr int S = J + 1;                      // metric scale 2^S
 };
 // |metric| relative to position 0's at the last renormalisation (every 16 stages), bounded by
 // (K-1)*(BMmax-BMmin) + 16*BMmax, must stay below 2^(22-S) (V in [2^23, 2^24) with t1/t2 margins):
 //   HARD 12+16 = 28 < 32;  SOFT4/FP32 192+256 = 448 < 8192;  SOFT8 3072+4096 = 7168 < 8192.
+// SOFT16 (int32): 6*131070 + 16*65536 = 1,834,996 < 2^21, so |V| < 2^30 and |V +- E| < 2^31.
 
 // branch-metric table: per 96-stage group, 16 periods of 6 rows (row K = stage phase); a row holds
 // BM[L]*2^S + c*2^j for the four labels L.  M_B32 rows of phase 0 hold a second set with the other
@@ -192,6 +197,69 @@ __device__ __forceinline__ void tg_stage_lds(float& V, f2v e, float vp, bool upp
         : "+{v60}"(V), "=&v"(t1), "=&v"(t2) : "v"(m), "v"(vp));
 }
 
+// int32 stages (TgFmt::INT): the same three forms on integer patterns
+// two-op form: a = V + m, b = V - m, V' = max(a, b of the partner) -- the partner has the same label and
+// tag outside M_B32's phase-0 rows, so its b is this lane's exchanged candidate
+template <int Q>
+__device__ __forceinline__ void tg_stage_dpp_i2(float& V, float m)
+{
+    float a, b;
+#define VD_TG_DPPI2(CTRL)                                                                                  \
+    asm("v_sub_u32 %2, %0, %3\n\tv_add_u32 %1, %0, %3\n\ts_nop 0\n\tv_max_i32_dpp %0, %2, %1 " CTRL            \
+        " row_mask:0xf bank_mask:0xf"                                                                      \
+        : "+{v60}"(V), "=&v"(a), "=&v"(b) : "v"(m))
+    if constexpr (Q == 0) VD_TG_DPPI2("quad_perm:[1,0,3,2]");
+    else if constexpr (Q == 1) VD_TG_DPPI2("quad_perm:[2,3,0,1]");
+    else if constexpr (Q == 2) VD_TG_DPPI2("row_half_mirror");
+    else VD_TG_DPPI2("row_ror:8");
+#undef VD_TG_DPPI2
+}
+// FM (study, ABL 1<<22): the max on the patterns as fp32 (patterns kept positive normal floats)
+template <int Q, bool FM = false>
+__device__ __forceinline__ void tg_stage_dpp_i(float& V, float m)
+{
+    float t1, t2;
+#define VD_TG_DPPI(CTRL)                                                                                  \
+    if constexpr (FM)                                                                                     \
+    asm("v_add_u32 %1, %0, %3\n\ts_nop 0\n\tv_sub_u32_dpp %2, %0, %3 " CTRL " row_mask:0xf bank_mask:0xf\n\t" \
+        "v_max_f32 %0, %1, %2"                                                                           \
+        : "+{v60}"(V), "=&v"(t1), "=&v"(t2) : "v"(m));                                                   \
+    else                                                                                                  \
+    asm("v_add_u32 %1, %0, %3\n\ts_nop 0\n\tv_sub_u32_dpp %2, %0, %3 " CTRL " row_mask:0xf bank_mask:0xf\n\t" \
+        "v_max_i32 %0, %1, %2"                                                                           \
+        : "+{v60}"(V), "=&v"(t1), "=&v"(t2) : "v"(m))
+    if constexpr (Q == 0) VD_TG_DPPI("quad_perm:[1,0,3,2]");
+    else if constexpr (Q == 1) VD_TG_DPPI("quad_perm:[2,3,0,1]");
+    else if constexpr (Q == 2) VD_TG_DPPI("row_half_mirror");
+    else VD_TG_DPPI("row_ror:8");
+#undef VD_TG_DPPI
+}
+// xor-32 swap stage: e = this lane's signed pair, (E-, -E+) in the lower position half, (-E-, E+) in the
+// upper one, so both halves form [a, b] = [V + e.x, V + e.y] and swap as the fp32 stage does
+template <bool FM = false>
+__device__ __forceinline__ void tg_stage_swap_i(float& V, f2v e)
+{
+    if constexpr (FM)
+        asm("v_add_u32 v62, %0, %1\n\tv_add_u32 v63, %0, %2\n\ts_nop 1\n\tv_permlane32_swap_b32 v62, v63\n\t"
+            "v_max_f32 %0, v62, v63"
+            : "+{v60}"(V) : "v"(e.x), "v"(e.y) : "v62", "v63");
+    else
+        asm("v_add_u32 v62, %0, %1\n\tv_add_u32 v63, %0, %2\n\ts_nop 1\n\tv_permlane32_swap_b32 v62, v63\n\t"
+            "v_max_i32 %0, v62, v63"
+            : "+{v60}"(V) : "v"(e.x), "v"(e.y) : "v62", "v63");
+}
+template <bool FM = false>
+__device__ __forceinline__ void tg_stage_lds_i(float& V, float m, float vp)
+{
+    float t1, t2;
+    if constexpr (FM)
+        asm("v_add_u32 %1, %0, %3\n\tv_sub_u32 %2, %4, %3\n\tv_max_f32 %0, %1, %2"
+            : "+{v60}"(V), "=&v"(t1), "=&v"(t2) : "v"(m), "v"(vp));
+    else
+        asm("v_add_u32 %1, %0, %3\n\tv_sub_u32 %2, %4, %3\n\tv_max_i32 %0, %1, %2"
+            : "+{v60}"(V), "=&v"(t1), "=&v"(t2) : "v"(m), "v"(vp));
+}
+
 // ---------------------------------------------------------------- group traceback (reference viterbiTB.cuh:4-21)
 // Ring slot = 64 words indexed by position; byte/half g of word p holds the take-bits of history field
 // g along the survivor ending at p (register exchange within the field).  Tracing word k from state
@@ -312,6 +380,24 @@ struct TgIn<SOFT8> {  // 2 stages per word; the 16-bit half g^1 holds s0 (high b
     }
 };
 template <>
+struct TgIn<SOFT16> {  // 1 stage per word: high 16 bits s0, low 16 bits s1
+    using raw_t = uint32_t;
+    static constexpr int RB = 128;
+    static __device__ __forceinline__ uint64_t bytes(uint64_t stages) { return stages * 4; }
+    static __device__ __forceinline__ uint32_t voff(int li) { return 4u * (uint32_t)li; }
+    template <int R>
+    static __device__ __forceinline__ raw_t load(__amdgpu_buffer_rsrc_t rs, uint32_t vo)
+    {
+        return __builtin_amdgcn_raw_buffer_load_b32(rs, vo + R * RB, 0, 0);
+    }
+    static __device__ __forceinline__ void ab(raw_t w, int, int& A, int& B, float)
+    {
+        const int s0 = (int)w >> 16, s1 = (int)(w << 16) >> 16;
+        A = s0 + s1;
+        B = s0 - s1;
+    }
+};
+template <>
 struct TgIn<FP32> {  // 2 floats per stage, clamped to [-8,7]; BM = (int)(+-x0 +- x1) (truncation)
     using raw_t = float2;
     static constexpr int RB = 256;
@@ -363,6 +449,7 @@ struct TgInLlr {
 template <> struct TgIn<kLlr + HARD> : TgInLlr<HARD> {};
 template <> struct TgIn<kLlr + SOFT4> : TgInLlr<SOFT4> {};
 template <> struct TgIn<kLlr + SOFT8> : TgInLlr<SOFT8> {};
+template <> struct TgIn<kLlr + SOFT16> : TgInLlr<SOFT16> {};
 template <> struct TgIn<kLlr + FP32> : TgInLlr<FP32> {};
 // resource for the 96 stages from g0 (g0 a multiple of 16).
 // The range min(max(availBytes - off, 0), 2^32 - 1) is computed on the scalar unit with 32-bit halves
@@ -447,6 +534,9 @@ template <int CH, int CORE, int OB, int ABL = 0>
 __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(7))) void vd_decode_tg(const void* __restrict__ in, void* __restrict__ out, Geom geo)
 {
     using IN = TgIn<CH>;
+    constexpr bool INT = TgFmt<CH>::INT;
+    static_assert(!INT || CORE == B32, "int32 patterns: SOFT16 on the int32 core only");
+    constexpr bool FM = INT && (ABL & (1 << 22));  // study: signed max on the patterns as fp32
     using TT = TgTab<CORE>;
     constexpr int J = TgFmt<CH>::J, S = TgFmt<CH>::S;
     constexpr int TBS = TgRing<CORE>::TBS;
@@ -473,13 +563,18 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(7))
     // per-lane LDS byte addresses of this position's table entries (row offsets are compile-time)
     // per-lane LDS byte offset of this position's entry in a phase-K row (row offsets are compile-time);
     // [sx, -sx] route the swap stages' candidates (see tg_stage_swap and the file header)
+    const bool upper5 = (pos >> 5) & 1;
     int aK[6];
     sfor<6>([&](auto KK) {
         constexpr int K = decltype(KK)::value;
         aK[K] = 8 * own_label(pos, K);
     });
+    // INT phase-0 swap stage: this lane's signed pair, read as two dwords of the (E-, E+) pair row:
+    // (E-[L], -E+[L]) = (E-[L], E-[3-L]) in the lower position half, (-E-[L], E+[L]) = (E+[3-L], E+[L]) in
+    // the upper one (BM[3-L] = -BM[L])
+    const int L0 = own_label(pos, 0);
+    const int aPx = upper5 ? 8 * (3 - L0) + 4 : 8 * L0, aPy = upper5 ? 8 * L0 + 4 : 8 * (3 - L0);
     const int pa5 = 4 * (lane ^ 32);  // ds_bpermute address of the xor-32 partner (tools variant)
-    const bool upper5 = (pos >> 5) & 1;
     const f2v spm = (f2v){1.0f, -1.0f};  // [a, b] = [V + m, V - m] of the two-op DPP stage
     f2v sxp[2];
     sfor<2>([&](auto W) {
@@ -497,7 +592,9 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(7))
     // V lives in [2^23, 2^24), where the fp32 ulp is 1 and the low mantissa bits ARE the low integer
     // bits: V = 1.5*2^23 + metric*2^S + 2^(S-1) + h.  The 2^(S-1) offset keeps the history field
     // 2^(S-1) + h in (0, 2^S), so read-out and clearing are bit operations on the pattern.
-    constexpr uint32_t VBASE = 0x4B400000u + (1u << (S - 1));  // pattern of 1.5*2^23 + 2^(S-1)
+    // INT: V = metric*2^S + 2^(S-1) + h as an int32, no base needed.
+    // FM: base 2^30 keeps every pattern and candidate in [2^23, 2^31 - 2^23) (|V - base| < 2^30 * 0.91).
+    constexpr uint32_t VBASE = (INT ? (FM ? 0x40000000u : 0u) : 0x4B400000u) + (1u << (S - 1));  // pattern of 1.5*2^23 + 2^(S-1)
     const uint32_t fnm = ~((1u << S) - 1u), fhf = 1u << (S - 1);  // field clear: (p & fnm) | fhf
     Fair<(ABL & (1 << 20)) != 0> fair;  // fairness controller (vd_kernels.h; ABL & 256 disables)
     if constexpr (!(ABL & 256)) fair.begin(geo.fair, lane);
@@ -550,6 +647,9 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(7))
         constexpr int r = decltype(Rc)::value;  // stage within the group (the group starts at phase 0)
         constexpr int K = r % 6;
         if constexpr (ABL & 2) {
+        } else if constexpr (INT && TT::pairrow(K)) {
+            typedef __attribute__((address_space(3))) const volatile float* lptr1;
+            vp[r] = (f2v){*(lptr1)(tl + aPx + TT::row(r)), *(lptr1)(tl + aPy + TT::row(r))};
         } else if constexpr (TT::pairrow(K) || (r / 6) % 2 == 0) {
             vp[r] = *(lptr)(tl + aK[K] + TT::row(r));
         }
@@ -575,7 +675,24 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(7))
             constexpr bool IS16 = Q == X16, IS32 = Q == 5;
             constexpr int DCTRL = MAPB && Q == 4 ? 2 : (Q <= 3 ? Q : 3);  // lane xor 1, 2, 7, 8 -> DPP control
             constexpr bool LSW = (IS32 && (ABL & 8192)) || (IS16 && !(ABL & 16384));
-            if constexpr (((!IS16 && !IS32) || (ABL & 128)) && (ABL & (262144 | 524288)) && !TT::pairrow(K)) {
+            if constexpr (INT && (ABL & (1 << 23))) {  // study: the fp32 stages on the int patterns (wrong results)
+                if constexpr (Q <= 3) tg_stage_dpp<Q>(V, ODD ? vp[RP].y : vp[RP].x);
+                else if constexpr (Q == 5) tg_stage_swap<5, 2>(V, vp[RP], sxp[0]);
+                else {
+                    const float pv = __builtin_bit_cast(float, __builtin_amdgcn_ds_swizzle(__builtin_bit_cast(int, V), 0x401F));
+                    tg_stage_lds<0>(V, vp[RP], pv, upper5);
+                }
+            } else if constexpr (INT) {  // int32 patterns (SOFT16): DPP, xor-32 swap (signed pairs), xor-16 swizzle
+                // DPP stages in the two-op form (sub, add, max with the partner's b through DPP): 5 %
+                // faster than add, sub_dpp, max on int32 (tools/vd_ablate; ABL 1<<24: the three-op form)
+                if constexpr (Q <= 3 && !(ABL & (1 << 24))) tg_stage_dpp_i2<Q>(V, ODD ? vp[RP].y : vp[RP].x);
+                else if constexpr (Q <= 3) tg_stage_dpp_i<Q, FM>(V, ODD ? vp[RP].y : vp[RP].x);
+                else if constexpr (Q == 5) tg_stage_swap_i<FM>(V, vp[RP]);
+                else {
+                    const float pv = __builtin_bit_cast(float, __builtin_amdgcn_ds_swizzle(__builtin_bit_cast(int, V), 0x401F));
+                    tg_stage_lds_i<FM>(V, ODD ? vp[RP].y : vp[RP].x, pv);
+                }
+            } else if constexpr (((!IS16 && !IS32) || (ABL & 128)) && (ABL & (262144 | 524288)) && !TT::pairrow(K)) {
                 // ABL (tools only): 262144 = sub, add, max_dpp; 524288 = pk_fma, max_dpp
                 const f2v e = (ABL & 2) ? (f2v){(float)aK[K], 1.0f} : vp[RP];
                 tg_stage_dpp2<DCTRL, ODD ? 1 : 0, (ABL & 524288) != 0>(V, e, spm);
@@ -656,6 +773,21 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(7))
     // table row of stage phase K: E[L] = BM[L]*2^S + tag at entries 0, 2, 4, 6 (the odd dwords are the
     // other period's); M_B32 phase-0 rows: the pairs (E-[L], E+[L]) of both tag signs
     auto put_row = [&](int rb, int A, int B, int K) {
+        if constexpr (INT) {  // int32 entries, the fp32 layout (phase-0 rows: the pairs (E-[L], E+[L]))
+            uint32_t* e = (uint32_t*)(tabb + rb);
+            const int a = A * (1 << S), b = B * (1 << S), tag = 1 << (lane % J);
+            e[0] = (uint32_t)(-a - tag);
+            e[2] = (uint32_t)(-b - tag);
+            e[4] = (uint32_t)(b - tag);
+            e[6] = (uint32_t)(a - tag);
+            if (K == 0) {
+                e[1] = (uint32_t)(-a + tag);
+                e[3] = (uint32_t)(-b + tag);
+                e[5] = (uint32_t)(b + tag);
+                e[7] = (uint32_t)(a + tag);
+            }
+            return;
+        }
         constexpr float SC = (float)(1 << S);
         const float af = (float)A, bf = (float)B;
         float* e = (float*)(tabb + rb);

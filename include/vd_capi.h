@@ -107,7 +107,7 @@ int vd_run_stream(vd_decoder* dec, const void* const* input_h, void* const* outp
  * device (a trailing partial word packs missing values as 0.0f). */
 int vd_pack_device(int options, const float* llr_d, size_t inputNum, float scale, void* packed_d, void* stream);
 /* Fused quantise + decode from device floats: the branch-metric table build quantises each value
- * (no packed intermediate, one kernel).  SOFT16 packs into the decoder's buffer first. */
+ * (no packed intermediate, one kernel), every format. */
 int vd_run_device_llr(vd_decoder* dec, const float* llr_d, void* output_d, size_t inputNum, float scale,
                       void* stream);
 /* Blocking host-to-host variant (H2D of the floats, fused decode, D2H); kernel_ms as in vd_run. */

@@ -69,6 +69,33 @@ def test_parity_long_chunks(gpu, vo, opt):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("opt", VALID, ids=name)
+def test_parity_full_range_inputs(gpu, vo, opt):
+    # random channel words over each format's whole range (every soft value and sign combination, FP32
+    # values from +-2^-10 to +-2^20 incl. exact integers and the clamp limits): the branch metrics span
+    # [BMmin, BMmax], so the path-metric spread reaches the bound the tagged kernels are sized for
+    # (vd_kernel_tg.h TgFmt; SOFT16's int32 patterns in particular)
+    rng = np.random.default_rng(opt + 99)
+    n = 2_000_000  # encoded values (1M bits)
+    nbytes = gpu.lib().vd_input_size(opt, n)
+    if (opt & 0xF) == FP32:
+        mag = np.exp2(rng.uniform(-10, 20, n)).astype(np.float32)
+        small = rng.random(n) < 0.2  # exact small integers, where the truncation to int decides
+        mag[small] = rng.integers(0, 9, int(small.sum())).astype(np.float32)
+        vals = np.where(rng.random(n) < 0.5, -mag, mag).astype(np.float32)
+        vals[::97] = 7.0
+        vals[1::97] = -8.0
+        packed = vals
+    else:
+        packed = rng.integers(0, 2 ** 32, nbytes // 4, dtype=np.uint64).astype(np.uint32).view(np.int32)
+    ref, ok = vo.decode(opt, packed, input_num=n)
+    assert ok
+    out = gpu_decode(gpu, opt, packed, input_num=n)
+    bad = np.flatnonzero(out != ref)
+    assert bad.size == 0, f"{bad.size} words differ, first at {bad[:5]}"
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("n_bits", [160, 2_048, 3_008, 204_800, 206_400, 409_616, 1_000_016])
 @pytest.mark.parametrize("opt", [HARD | M_B32, SOFT8 | M_B16 | O_B16, FP32 | M_FP16], ids=name)
 def test_parity_ragged_and_empty_chunks(gpu, vo, opt, n_bits):
@@ -137,6 +164,19 @@ def test_o_b16_known_answer_within_race(gpu, vo):
 def test_parity_full_32m(gpu, vo, opt):
     # BASELINE configs 2 and 3 at full size, every word checked against the oracle
     bits, packed = vo.simulate(opt, 32_000_000, 1.2, 1, 2)
+    ref, ok = vo.decode(opt, packed, nthreads=16)
+    assert ok
+    out = gpu_decode(gpu, opt, packed)
+    np.testing.assert_array_equal(out, ref)
+    assert gpu.count_errors(opt, bits, out) == vo.ben(opt, bits, ref)
+
+
+@pytest.mark.gpu
+@pytest.mark.slow
+def test_parity_full_32m_soft16(gpu, vo):
+    # 32M bits of 16-bit soft input on the int32-pattern tagged kernel, every word against the oracle
+    opt = SOFT16 | M_B32
+    bits, packed = vo.simulate(opt, 32_000_000, 1.2, 5, 6)
     ref, ok = vo.decode(opt, packed, nthreads=16)
     assert ok
     out = gpu_decode(gpu, opt, packed)

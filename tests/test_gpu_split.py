@@ -9,7 +9,7 @@ import os
 import numpy as np
 import pytest
 
-from vitdec import FP32, HARD, M_B16, M_B32, M_FP16, SOFT4, SOFT8
+from vitdec import FP32, HARD, M_B16, M_B32, M_FP16, SOFT4, SOFT8, SOFT16
 from test_gpu_parity import gpu_decode, name
 
 
@@ -26,7 +26,7 @@ def decode_split_and_whole(gpu, opt, packed, n):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("opt", [HARD | M_B32, SOFT8 | M_B16, SOFT4 | M_B32, FP32 | M_FP16], ids=name)
+@pytest.mark.parametrize("opt", [HARD | M_B32, SOFT8 | M_B16, SOFT4 | M_B32, FP32 | M_FP16, SOFT16 | M_B32], ids=name)
 @pytest.mark.parametrize("snr", [0.0, 1.0, 3.0])
 def test_split_equals_whole_16m(gpu, vo, opt, snr):
     n = 16_000_000  # 78 words per chunk: split (>= 64)

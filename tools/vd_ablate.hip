@@ -7,7 +7,7 @@
 #include <vector>
 #include <algorithm>
 #include <cstring>
-#include "../gpu-accelerated-viterbi-decoder_amd/csrc/vd_kernels.h"
+#include "vd_sc_kernel.h"
 #include "../gpu-accelerated-viterbi-decoder_amd/csrc/vd_kernel_tg.h"
 #include "vd_pk_kernel.h"
 
@@ -21,6 +21,7 @@ template <int ABL> void adds(std::vector<Var>& v, const char* n) { v.push_back({
 template <int ABL> void tgb(std::vector<Var>& v, const char* n) { v.push_back({n, (KFn)vd::vd_decode_tg<vd::HARD, vd::B32, 32, ABL>, 1600}); }
 template <int ABL> void tgs(std::vector<Var>& v, const char* n) { v.push_back({n, (KFn)vd::vd_decode_tg<vd::SOFT8, vd::B16, 32, ABL>, 1600}); }
 template <int ABL> void tgf(std::vector<Var>& v, const char* n) { v.push_back({n, (KFn)vd::vd_decode_tg<vd::FP32, vd::F16, 32, ABL>, 1600}); }
+template <int ABL> void tgi(std::vector<Var>& v, const char* n) { v.push_back({n, (KFn)vd::vd_decode_tg<vd::SOFT16, vd::B32, 32, ABL>, 1600}); }
 template <int ABL> void addp(std::vector<Var>& v, const char* n) { v.push_back({n, (KFn)vd::vd_decode_pk<vd::SOFT8, vd::B16, 32, ABL>, 3200, 64}); }
 
 int main(int argc, char** argv)
@@ -46,6 +47,12 @@ int main(int argc, char** argv)
     tgb<0>(v, "tg hard/b32 full"); tgb<1>(v, "tg hard/b32 -traceback"); tgb<16>(v, "tg hard/b32 -loads"); tgb<256>(v, "tg hard/b32 -fairness");
     tgb<2>(v, "tg hard/b32 -tabreads"); tgb<4>(v, "tg hard/b32 -readout"); tgb<8>(v, "tg hard/b32 -tabbuild"); tgb<128>(v, "tg hard/b32 all-dpp"); tgb<512>(v, "tg hard/b32 -tabwrites"); tgs<512>(v, "tg soft8/b16 -tabwrites"); tgs<8>(v, "tg soft8/b16 -tabbuild");
     tgb<2 | 4 | 8 | 16 | 1>(v, "tg hard/b32 ACS only"); tgb<2 | 4 | 8 | 16 | 1 | 128>(v, "tg hard/b32 ACS only all-dpp");
+    tgs<2 | 4 | 8 | 16 | 1>(v, "tg soft8/b16 ACS only");
+    tgi<0>(v, "tg soft16/b32 full"); tgi<(1 << 22)>(v, "tg soft16/b32 fp32 max");
+    tgi<(1 << 23)>(v, "tg soft16/b32 fp32 stages"); tgi<8>(v, "tg soft16/b32 -tabbuild"); tgi<4>(v, "tg soft16/b32 -readout");
+    tgi<1>(v, "tg soft16/b32 -traceback"); tgi<2 | 4 | 8 | 16 | 1>(v, "tg soft16/b32 ACS only");
+    tgi<2 | 4 | 8 | 16 | 1 | (1 << 23)>(v, "tg soft16/b32 ACS only fp32");
+    tgi<(1 << 24)>(v, "tg soft16/b32 dpp three-op");
     tgs<0>(v, "tg soft8/b16 full"); tgs<1>(v, "tg soft8/b16 -traceback"); tgs<2>(v, "tg soft8/b16 -tabreads"); tgs<4>(v, "tg soft8/b16 -readout"); tgf<0>(v, "tg fp32/f16 full");
     tgb<262144>(v, "tg hard/b32 sub+add+maxdpp"); tgs<262144>(v, "tg soft8/b16 sub+add+maxdpp");
     tgb<524288>(v, "tg hard/b32 pkfma+maxdpp"); tgs<524288>(v, "tg soft8/b16 pkfma+maxdpp");
@@ -57,6 +64,7 @@ int main(int argc, char** argv)
         for (size_t i = 0; i < v.size(); i++) { if (!strcmp(v[i].name, a)) ia = (int)i; if (!strcmp(v[i].name, b)) ib = (int)i; }
         if (ia >= 0 && ib >= 0) v[ib].ref = ia;
     };
+    twin("tg soft16/b32 full", "tg soft16/b32 fp32 max"); twin("tg soft16/b32 full", "tg soft16/b32 dpp three-op");
     for (const char* k : {"sub+add+maxdpp", "pkfma+maxdpp", "board sc1 loads", "dpp no inner nop"}) {
         char a[96], b[96];
         snprintf(a, sizeof a, "tg hard/b32 full"); snprintf(b, sizeof b, "tg hard/b32 %s", k); twin(a, b);

@@ -7,7 +7,7 @@
 #include <cstdio>
 #include <vector>
 #include <algorithm>
-#include "../gpu-accelerated-viterbi-decoder_amd/csrc/vd_kernels.h"
+#include "vd_sc_kernel.h"
 
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP %s line %d\n", hipGetErrorString(e), __LINE__); return 1; } } while (0)
 
