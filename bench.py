@@ -449,31 +449,35 @@ def main():
     torch.cuda.synchronize()
 
     nw = len(batches)
-    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(nw + 1)] for _ in range(args.steps)]
+    # The K steps' launches go out back to back on one stream, grouped by workload (all K batches of
+    # workload 0, then all of workload 1, ...): every batch is independent, so the order inside the timed
+    # region does not change the work, and one HIP event between the groups times each kernel over its K
+    # launches.  An event recorded between two kernels costs the GPU a ~5 us bubble (rocprofv3 kernel
+    # trace, profiles/r02), so per-launch events would both slow the step and inflate the kernel times.
+    evs = [torch.cuda.Event(enable_timing=True) for _ in range(nw + 1)]
 
-    def step(ev=None):
-        if ev is not None:
-            ev[0].record(stream)
-        for i, b in enumerate(batches):
-            b["dec"].run_device(b["inp"].data_ptr(), b["out"].data_ptr(), b["input_num"], sptr)
-            if ev is not None:
-                ev[i + 1].record(stream)
+    def run(b):
+        b["dec"].run_device(b["inp"].data_ptr(), b["out"].data_ptr(), b["input_num"], sptr)
 
     for _ in range(args.warmup):
-        step()
+        for b in batches:
+            run(b)
     if world > 1:
         torch.distributed.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for s in range(args.steps):
-        step(evs[s])
+    evs[0].record(stream)
+    for i, b in enumerate(batches):
+        for _ in range(args.steps):
+            run(b)
+        evs[i + 1].record(stream)
     torch.cuda.synchronize()
     if world > 1:
         torch.distributed.barrier()
     elapsed = time.perf_counter() - t0
 
-    # per-kernel average durations from HIP events on the launch stream
-    kms = [float(np.mean([evs[s][i].elapsed_time(evs[s][i + 1]) for s in range(args.steps)])) for i in range(nw)]
+    # per-kernel average durations from the HIP events on the launch stream
+    kms = [evs[i].elapsed_time(evs[i + 1]) / args.steps for i in range(nw)]
 
     # correctness side-channel (outside the timed region): BER of each batch vs its source bits,
     # and an RCCL all_gather of per-rank decoded-word checksums (the only cross-GPU traffic)
@@ -543,6 +547,7 @@ def main():
                 "decoded_bits_per_batch": batches[0]["msg"],
                 "parallelism": f"batch-shard x{world}" if world > 1 else "single GPU",
                 "kernel_ms": {b["name"]: round(k, 4) for b, k in zip(batches, kms)},
+                "step_minus_kernels_us": round((ms_per_step - sum(kms)) * 1e3, 2),
                 "kernel_gbps": {b["name"]: round(b["msg"] / (k * 1e-3) / 1e9, 2) for b, k in zip(batches, kms)},
                 "ber": {b["name"]: bers[i] for i, b in enumerate(batches)},
                 "kernels": {b["name"]: vitdec.kernel_name(b["opt"]) for b in batches},

@@ -9,6 +9,7 @@
 #include <cstring>
 #include "vd_sc_kernel.h"
 #include "../gpu-accelerated-viterbi-decoder_amd/csrc/vd_kernel_tg.h"
+#include "../gpu-accelerated-viterbi-decoder_amd/csrc/vd_kernel_ps.h"
 #include "vd_pk_kernel.h"
 
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP error %s at %d\n", hipGetErrorString(e), __LINE__); exit(1); } } while (0)
@@ -22,6 +23,7 @@ template <int ABL> void tgb(std::vector<Var>& v, const char* n) { v.push_back({n
 template <int ABL> void tgs(std::vector<Var>& v, const char* n) { v.push_back({n, (KFn)vd::vd_decode_tg<vd::SOFT8, vd::B16, 32, ABL>, 1600}); }
 template <int ABL> void tgf(std::vector<Var>& v, const char* n) { v.push_back({n, (KFn)vd::vd_decode_tg<vd::FP32, vd::F16, 32, ABL>, 1600}); }
 template <int ABL> void tgi(std::vector<Var>& v, const char* n) { v.push_back({n, (KFn)vd::vd_decode_tg<vd::SOFT16, vd::B32, 32, ABL>, 1600}); }
+template <int CH, int CORE, int ABL> void psk(std::vector<Var>& v, const char* n) { v.push_back({n, (KFn)vd::vd_decode_ps<CH, CORE, 32, ABL>, 800}); }
 template <int ABL> void addp(std::vector<Var>& v, const char* n) { v.push_back({n, (KFn)vd::vd_decode_pk<vd::SOFT8, vd::B16, 32, ABL>, 3200, 64}); }
 
 int main(int argc, char** argv)
@@ -53,6 +55,15 @@ int main(int argc, char** argv)
     tgi<1>(v, "tg soft16/b32 -traceback"); tgi<2 | 4 | 8 | 16 | 1>(v, "tg soft16/b32 ACS only");
     tgi<2 | 4 | 8 | 16 | 1 | (1 << 23)>(v, "tg soft16/b32 ACS only fp32");
     tgi<(1 << 24)>(v, "tg soft16/b32 dpp three-op");
+    psk<vd::HARD, vd::B32, 0>(v, "ps hard/b32 full"); psk<vd::SOFT8, vd::B16, 0>(v, "ps soft8/b16 full");
+    psk<vd::SOFT16, vd::B32, 0>(v, "ps soft16/b32 full"); psk<vd::FP32, vd::F16, 0>(v, "ps fp32/f16 full");
+    psk<vd::SOFT8, vd::B16, 1>(v, "ps soft8/b16 -traceback"); psk<vd::SOFT8, vd::B16, 2>(v, "ps soft8/b16 -tabreads");
+    psk<vd::SOFT8, vd::B16, 4>(v, "ps soft8/b16 -readout"); psk<vd::SOFT8, vd::B16, 8>(v, "ps soft8/b16 -tabbuild");
+    psk<vd::SOFT8, vd::B16, 16>(v, "ps soft8/b16 -loads"); psk<vd::SOFT8, vd::B16, 256>(v, "ps soft8/b16 -fairness");
+    psk<vd::SOFT8, vd::B16, 1 | 2 | 4 | 8 | 16>(v, "ps soft8/b16 ACS only");
+    // balanced grids (every SIMD the same waves): 6144 chunks; the rate is per 6144-chunk launch
+    v.push_back({"tg soft8/b16 6144 chunks", (KFn)vd::vd_decode_tg<vd::SOFT8, vd::B16, 32, 0>, 1536});
+    v.push_back({"ps soft8/b16 6144 chunks", (KFn)vd::vd_decode_ps<vd::SOFT8, vd::B16, 32, 0>, 768});
     tgs<0>(v, "tg soft8/b16 full"); tgs<1>(v, "tg soft8/b16 -traceback"); tgs<2>(v, "tg soft8/b16 -tabreads"); tgs<4>(v, "tg soft8/b16 -readout"); tgf<0>(v, "tg fp32/f16 full");
     tgb<262144>(v, "tg hard/b32 sub+add+maxdpp"); tgs<262144>(v, "tg soft8/b16 sub+add+maxdpp");
     tgb<524288>(v, "tg hard/b32 pkfma+maxdpp"); tgs<524288>(v, "tg soft8/b16 pkfma+maxdpp");
@@ -65,6 +76,8 @@ int main(int argc, char** argv)
         if (ia >= 0 && ib >= 0) v[ib].ref = ia;
     };
     twin("tg soft16/b32 full", "tg soft16/b32 fp32 max"); twin("tg soft16/b32 full", "tg soft16/b32 dpp three-op");
+    twin("tg hard/b32 full", "ps hard/b32 full"); twin("tg soft8/b16 full", "ps soft8/b16 full");
+    twin("tg soft16/b32 full", "ps soft16/b32 full"); twin("tg fp32/f16 full", "ps fp32/f16 full");
     for (const char* k : {"sub+add+maxdpp", "pkfma+maxdpp", "board sc1 loads", "dpp no inner nop"}) {
         char a[96], b[96];
         snprintf(a, sizeof a, "tg hard/b32 full"); snprintf(b, sizeof b, "tg hard/b32 %s", k); twin(a, b);
