@@ -21,7 +21,6 @@
 #include "../../include/vd_capi.h"
 #include "vd_kernels.h"
 #include "vd_kernel_tg.h"
-#include "vd_kernel_ps.h"
 #include "vd_pack.h"
 #include "vd_mt.h"
 #include "vd_mtjump.h"
@@ -98,75 +97,56 @@ uint64_t avail_stages(int o, size_t n)
 
 using launch_fn = void (*)(const void*, void*, vd::Geom, hipStream_t);
 
-// Two kernel families, same decoded words: 0 = vd_decode_tg (one state per lane, one chunk per wave,
-// 4-wave workgroups), 1 = vd_decode_ps (two states per lane, two chunks per wave, 8 chunk slots per
-// 4-wave workgroup).  VD_KERNEL=tg / ps at vd_create selects one.
-constexpr int kFamTg = 0, kFamPs = 1;
-
 // workgroups of a launch: whole-chunk workgroups plus one per split chunk
 unsigned tg_grid(const vd::Geom& g)
 {
     if (g.nwhole == 0) return (g.nchunks + vd::kWaves - 1) / vd::kWaves;
     return g.nwhole / vd::kWaves + (g.nchunks - g.nwhole);
 }
-unsigned ps_grid(const vd::Geom& g)
-{
-    if (g.nwhole == 0) return (g.nchunks + vd::kPsSlots - 1) / vd::kPsSlots;
-    return g.nwhole / vd::kPsSlots + (g.nchunks - g.nwhole);
-}
 
 // one kernel per format (SOFT16 on int32 patterns, TgFmt::INT); CH >= kLlr: float channel values
 // quantised in the table build (fused SoftDecisionPacker)
-template <int CH, int CORE, int OB, int FAM>
+template <int CH, int CORE, int OB>
 void launch_t(const void* in, void* out, vd::Geom g, hipStream_t s)
 {
-    if constexpr (FAM == kFamPs)
-        hipLaunchKernelGGL((vd::vd_decode_ps<CH, CORE, OB>), dim3(ps_grid(g)), dim3(64 * vd::kPsWaves), 0, s, in, out, g);
-    else
-        hipLaunchKernelGGL((vd::vd_decode_tg<CH, CORE, OB>), dim3(tg_grid(g)), dim3(64 * vd::kWaves), 0, s, in, out, g);
+    hipLaunchKernelGGL((vd::vd_decode_tg<CH, CORE, OB>), dim3(tg_grid(g)), dim3(64 * vd::kWaves), 0, s, in, out, g);
 }
 
-template <int CH, int CORE, int FAM>
+template <int CH, int CORE>
 launch_fn pick_ob(int ob)
 {
-    return ob == 1 ? &launch_t<CH, CORE, 16, FAM> : &launch_t<CH, CORE, 32, FAM>;
+    return ob == 1 ? &launch_t<CH, CORE, 16> : &launch_t<CH, CORE, 32>;
 }
 
-template <int FAM, int L>
-launch_fn pick_fam(int o)
+template <int L>
+launch_fn pick_ch(int o)
 {
     const int ch = ch_of(o), me = met_of(o), ob = out_of(o);
     switch (ch) {
-    case 0: return me == 0 ? pick_ob<L + 0, 0, FAM>(ob) : me == 1 ? pick_ob<L + 0, 1, FAM>(ob) : pick_ob<L + 0, 2, FAM>(ob);
-    case 1: return me == 0 ? pick_ob<L + 1, 0, FAM>(ob) : me == 1 ? pick_ob<L + 1, 1, FAM>(ob) : pick_ob<L + 1, 2, FAM>(ob);
-    case 2: return me == 0 ? pick_ob<L + 2, 0, FAM>(ob) : pick_ob<L + 2, 1, FAM>(ob);
-    case 3: return pick_ob<L + 3, 0, FAM>(ob);
-    case 4: return me == 0 ? pick_ob<L + 4, 0, FAM>(ob) : me == 1 ? pick_ob<L + 4, 1, FAM>(ob) : pick_ob<L + 4, 2, FAM>(ob);
+    case 0: return me == 0 ? pick_ob<L + 0, 0>(ob) : me == 1 ? pick_ob<L + 0, 1>(ob) : pick_ob<L + 0, 2>(ob);
+    case 1: return me == 0 ? pick_ob<L + 1, 0>(ob) : me == 1 ? pick_ob<L + 1, 1>(ob) : pick_ob<L + 1, 2>(ob);
+    case 2: return me == 0 ? pick_ob<L + 2, 0>(ob) : pick_ob<L + 2, 1>(ob);
+    case 3: return pick_ob<L + 3, 0>(ob);
+    case 4: return me == 0 ? pick_ob<L + 4, 0>(ob) : me == 1 ? pick_ob<L + 4, 1>(ob) : pick_ob<L + 4, 2>(ob);
     }
     return nullptr;
 }
-launch_fn pick(int o, int fam, bool llr)
+launch_fn pick(int o, bool llr)
 {
-    if (llr) return fam == kFamPs ? pick_fam<kFamPs, vd::kLlr>(o) : pick_fam<kFamTg, vd::kLlr>(o);
-    return fam == kFamPs ? pick_fam<kFamPs, 0>(o) : pick_fam<kFamTg, 0>(o);
+    return llr ? pick_ch<vd::kLlr>(o) : pick_ch<0>(o);
 }
 
-const char* kname(int o, int fam = kFamPs)
+const char* kname(int o)
 {
-    static const char* names[2][5][3] = {
-        {{"vd_decode_tg<HARD,B32>", "vd_decode_tg<HARD,B16>", "vd_decode_tg<HARD,F16>"},
-         {"vd_decode_tg<SOFT4,B32>", "vd_decode_tg<SOFT4,B16>", "vd_decode_tg<SOFT4,F16>"},
-         {"vd_decode_tg<SOFT8,B32>", "vd_decode_tg<SOFT8,B16>", "-"},
-         {"vd_decode_tg<SOFT16,B32> (int32 patterns)", "-", "-"},
-         {"vd_decode_tg<FP32,B32>", "vd_decode_tg<FP32,B16>", "vd_decode_tg<FP32,F16>"}},
-        {{"vd_decode_ps<HARD,B32>", "vd_decode_ps<HARD,B16>", "vd_decode_ps<HARD,F16>"},
-         {"vd_decode_ps<SOFT4,B32>", "vd_decode_ps<SOFT4,B16>", "vd_decode_ps<SOFT4,F16>"},
-         {"vd_decode_ps<SOFT8,B32>", "vd_decode_ps<SOFT8,B16>", "-"},
-         {"vd_decode_ps<SOFT16,B32> (int32 patterns)", "-", "-"},
-         {"vd_decode_ps<FP32,B32>", "vd_decode_ps<FP32,B16>", "vd_decode_ps<FP32,F16>"}},
+    static const char* names[5][3] = {
+        {"vd_decode_tg<HARD,B32>", "vd_decode_tg<HARD,B16>", "vd_decode_tg<HARD,F16>"},
+        {"vd_decode_tg<SOFT4,B32>", "vd_decode_tg<SOFT4,B16>", "vd_decode_tg<SOFT4,F16>"},
+        {"vd_decode_tg<SOFT8,B32>", "vd_decode_tg<SOFT8,B16>", "-"},
+        {"vd_decode_tg<SOFT16,B32> (int32 patterns)", "-", "-"},
+        {"vd_decode_tg<FP32,B32>", "vd_decode_tg<FP32,B16>", "vd_decode_tg<FP32,F16>"},
     };
     if (!valid(o)) return "-";
-    return names[fam][ch_of(o)][met_of(o)];
+    return names[ch_of(o)][met_of(o)];
 }
 
 }  // namespace
@@ -201,7 +181,6 @@ struct vd_decoder {
     hipStream_t s_in = nullptr, s_out = nullptr;
     DeviceState* ds = nullptr;  // the device's board / split state (looked up once, vd_create)
     bool split = true;          // split launches allowed (VD_NO_SPLIT=1 at vd_create: no)
-    int fam = 1;                // kernel family (VD_KERNEL=tg at vd_create: the one-state-per-lane kernel)
 };
 
 static int ensure_capacity(vd_decoder* d, size_t inBytes, size_t outBytes)
@@ -233,7 +212,7 @@ static int ensure_capacity(vd_decoder* d, size_t inBytes, size_t outBytes)
 //  * the re-decode counter (vd_split_redecodes).
 // A decoder looks it up once (vd_create), not per launch.
 constexpr int kSplitSlots = 32;
-constexpr int kSpecVecs = vd::kPsVecs > vd::kSplitVecs ? vd::kPsVecs : vd::kSplitVecs;  // per split chunk
+constexpr int kSpecVecs = vd::kSplitVecs;  // per split chunk
 struct DeviceState {
     uint32_t* board = nullptr;
     int nsimd = 0;
@@ -267,29 +246,15 @@ static DeviceState* device_state(int device)
     }
     return st[device];
 }
-// split the launch when the chunks leave a remainder of exactly one piece wave per SIMD (6400 chunks
-// on 1024 SIMDs: 6 whole chunks per SIMD + 256 chunks in 4 pieces) and the chunks are long enough
-// Split the launch when the whole chunks leave exactly one piece wave per SIMD:
-//  tg (one chunk per wave): 6400 chunks on 1024 SIMDs = 6 whole per SIMD + 256 chunks of 4 pieces;
-//  ps (two chunks per wave): 6 whole chunks (3 waves) per SIMD + 256 chunks of 8 pieces (one 4-wave
-//  workgroup each, one wave per SIMD), 4 workgroups per CU;
-// and only when the chunks are long enough.
-static void plan_split(vd::Geom& g, int options, DeviceState* x, int fam)
+// Split the launch when the whole chunks leave exactly one piece wave per SIMD (6400 chunks on 1024
+// SIMDs: 6 whole chunks per SIMD + 256 chunks in 4 pieces) and the chunks are long enough.
+static void plan_split(vd::Geom& g, int options, DeviceState* x)
 {
     if (out_of(options) != 0) return;  // O_B32 only
     if (g.packNum / g.nchunks < (uint64_t)vd::kSplitMinWords) return;
     const uint32_t nsimd = (uint32_t)x->nsimd;
-    uint32_t nwhole;
-    if (fam == kFamPs) {
-        const uint32_t round = 2 * nsimd, rem = g.nchunks % round;  // chunk slots of one wave per SIMD
-        nwhole = g.nchunks - rem;
-        if (rem == 0 || rem * (vd::kPsSlots / 2) != nsimd) return;
-        if (nwhole / vd::kPsSlots + rem > (uint32_t)(nsimd / 4) * 4) return;  // 4 workgroups per CU
-    } else {
-        const uint32_t perSimd = g.nchunks / nsimd, rem = g.nchunks % nsimd;
-        nwhole = g.nchunks - rem;
-        if (rem == 0 || rem * vd::kWaves != nsimd || perSimd + 1 > 7) return;
-    }
+    const uint32_t perSimd = g.nchunks / nsimd, rem = g.nchunks % nsimd, nwhole = g.nchunks - rem;
+    if (rem == 0 || rem * vd::kWaves != nsimd || perSimd + 1 > 7) return;
     const uint32_t slot = x->next.fetch_add(1) % kSplitSlots;
     g.nwhole = nwhole;
     g.spec = x->spec + (size_t)slot * x->maxSplit * kSpecVecs * 64;
@@ -301,7 +266,7 @@ static int launch_decode(const vd_decoder* d, const void* in_d, void* out_d, siz
                          bool llr = false, float scale = 1.0f)
 {
     const int options = d->options;
-    launch_fn f = pick(options, d->fam, llr);
+    launch_fn f = pick(options, llr);
     if (!f) return fail(VD_ERR_OPTIONS, "invalid options");
     size_t msg = message_len(options, inputNum);
     vd::Geom g;
@@ -311,7 +276,7 @@ static int launch_decode(const vd_decoder* d, const void* in_d, void* out_d, siz
     g.scale = scale;
     if (g.packNum == 0) return VD_OK;
     g.fair = d->ds->board;
-    if (d->split) plan_split(g, options, d->ds, d->fam);
+    if (d->split) plan_split(g, options, d->ds);
     f(in_d, out_d, g, s);
     VD_HIP(hipGetLastError());
     return VD_OK;
@@ -336,11 +301,7 @@ int vd_split_redecodes(int device, uint64_t* count)
     return VD_OK;
 }
 const char* vd_last_error(void) { return g_err.c_str(); }
-const char* vd_kernel_name(int options)
-{
-    const char* kern = std::getenv("VD_KERNEL");
-    return kname(options, (kern && std::strcmp(kern, "tg") == 0) ? kFamTg : kFamPs);
-}
+const char* vd_kernel_name(int options) { return kname(options); }
 
 int vd_device_count(void)
 {
@@ -368,8 +329,6 @@ int vd_create(int options, size_t preallocInputNum, int device, vd_decoder** out
     }
     const char* nosplit = std::getenv("VD_NO_SPLIT");
     d->split = !(nosplit && nosplit[0] == '1');
-    const char* kern = std::getenv("VD_KERNEL");
-    d->fam = (kern && std::strcmp(kern, "tg") == 0) ? kFamTg : kFamPs;
     if (hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreate(&d->ev0) != hipSuccess || hipEventCreate(&d->ev1) != hipSuccess) {
         vd_destroy(d);

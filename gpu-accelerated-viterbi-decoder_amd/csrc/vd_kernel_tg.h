@@ -540,6 +540,12 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(7))
     using TT = TgTab<CORE>;
     constexpr int J = TgFmt<CH>::J, S = TgFmt<CH>::S;
     constexpr int TBS = TgRing<CORE>::TBS;
+    // xor-32 (Q=5) exchange: the partner's metric through the LDS crossbar (ds_bpermute, then the DPP
+    // stage's three ops) on the B16 / F16 cores, v_permlane32_swap (pk_fma, swap, max) on M_B32, whose
+    // heavier LDS load (pair rows: more table reads and writes) turns the extra LDS round trip into a
+    // loss (tools/vd_ablate, profiles/r02/ablate_q5.log: SOFT8/B16 -5 %, HARD/B32 +4.5 %).  ABL 8192
+    // (tools) flips the choice.
+    constexpr bool BP5 = !INT && ((CORE == B32) == ((ABL & 8192) != 0));
     __shared__ __attribute__((aligned(16))) char tab_all[kWaves][TT::BYTES];
     __shared__ __attribute__((aligned(256))) uint32_t ring_all[kWaves][(TBS + 1) * 64];  // bit 31-s = stage s
     const int lane = threadIdx.x & 63;
@@ -574,6 +580,7 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(7))
     // the upper one (BM[3-L] = -BM[L])
     const int L0 = own_label(pos, 0);
     const int aPx = upper5 ? 8 * (3 - L0) + 4 : 8 * L0, aPy = upper5 ? 8 * L0 + 4 : 8 * (3 - L0);
+    const int aU0 = aK[0] + (upper5 ? 4 : 0);  // M_B32 phase-0 pair row: this lane's (E-, E+) half
     const int pa5 = 4 * (lane ^ 32);  // ds_bpermute address of the xor-32 partner (tools variant)
     const f2v spm = (f2v){1.0f, -1.0f};  // [a, b] = [V + m, V - m] of the two-op DPP stage
     f2v sxp[2];
@@ -647,6 +654,10 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(7))
         constexpr int r = decltype(Rc)::value;  // stage within the group (the group starts at phase 0)
         constexpr int K = r % 6;
         if constexpr (ABL & 2) {
+        } else if constexpr (BP5 && TT::pairrow(K)) {
+            // xor-32 stage through the LDS crossbar on M_B32's phase-0 rows: this lane's tag sign only
+            typedef __attribute__((address_space(3))) const volatile float* lptr1;
+            vp[r] = (f2v){*(lptr1)(tl + aU0 + TT::row(r)), 0.0f};
         } else if constexpr (INT && TT::pairrow(K)) {
             typedef __attribute__((address_space(3))) const volatile float* lptr1;
             vp[r] = (f2v){*(lptr1)(tl + aPx + TT::row(r)), *(lptr1)(tl + aPy + TT::row(r))};
@@ -667,14 +678,14 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(7))
             constexpr bool ODD = (r / 6) % 2 == 1;
             constexpr int RP = TT::pairrow(K) ? r : (ODD ? r - 6 : r);  // where this stage's pair was read
             // The position bit on lane xor 16 (Q=4; Q=2 with the ABL 131072 map) fetches the partner's
-            // metric through the LDS crossbar (ds_swizzle), Q=5 (xor 32) swaps candidates with
-            // v_permlane32_swap: a VALU lane swap costs two issue slots, the swizzle none, and doing both
-            // through the LDS queues them behind each other and the table reads (tools/vd_swapab).
-            // ABL (tools only): 16384 = xor 16 by v_permlane16_swap too, 8192 = Q=5 by ds_bpermute.
+            // metric through the LDS crossbar (ds_swizzle); Q=5 (xor 32) through ds_bpermute or with the
+            // v_permlane32_swap candidate swap (BP5 above): a VALU lane swap costs ~2 DPP ops of issue, the
+            // LDS exchange one round trip queued behind the table reads.
+            // ABL (tools only): 16384 = xor 16 by v_permlane16_swap too, 8192 = flip the Q=5 choice (BP5).
             constexpr int X16 = MAPB ? 2 : 4;
             constexpr bool IS16 = Q == X16, IS32 = Q == 5;
             constexpr int DCTRL = MAPB && Q == 4 ? 2 : (Q <= 3 ? Q : 3);  // lane xor 1, 2, 7, 8 -> DPP control
-            constexpr bool LSW = (IS32 && (ABL & 8192)) || (IS16 && !(ABL & 16384));
+            constexpr bool LSW = (IS32 && BP5) || (IS16 && !(ABL & 16384));
             if constexpr (INT && (ABL & (1 << 23))) {  // study: the fp32 stages on the int patterns (wrong results)
                 if constexpr (Q <= 3) tg_stage_dpp<Q>(V, ODD ? vp[RP].y : vp[RP].x);
                 else if constexpr (Q == 5) tg_stage_swap<5, 2>(V, vp[RP], sxp[0]);
@@ -705,7 +716,7 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(7))
                 const float pv = IS16 ? __builtin_bit_cast(float, __builtin_amdgcn_ds_swizzle(__builtin_bit_cast(int, V), 0x401F))
                                       : tg_partner(V, pa5);
                 const f2v e = (ABL & 2) ? (f2v){(float)aK[K], 1.0f} : vp[RP];
-                tg_stage_lds<TT::pairrow(K) ? 2 : (ODD ? 1 : 0)>(V, e, pv, upper5);
+                tg_stage_lds<TT::pairrow(K) ? (BP5 ? 0 : 2) : (ODD ? 1 : 0)>(V, e, pv, upper5);
             } else {
                 const f2v e = (ABL & 2) ? (f2v){(float)aK[K], 1.0f} : vp[RP];
                 tg_stage_swap<IS16 ? 4 : 5, TT::pairrow(K) ? 2 : (ODD ? 1 : 0), (ABL >> 10) & 7>(V, e, sxp[K == 0 ? 0 : 1]);

@@ -7,9 +7,10 @@
 #include <vector>
 #include <algorithm>
 #include <cstring>
+#include <string>
 #include "vd_sc_kernel.h"
 #include "../gpu-accelerated-viterbi-decoder_amd/csrc/vd_kernel_tg.h"
-#include "../gpu-accelerated-viterbi-decoder_amd/csrc/vd_kernel_ps.h"
+#include "vd_ps_kernel.h"
 #include "vd_pk_kernel.h"
 
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP error %s at %d\n", hipGetErrorString(e), __LINE__); exit(1); } } while (0)
@@ -61,6 +62,7 @@ int main(int argc, char** argv)
     psk<vd::SOFT8, vd::B16, 4>(v, "ps soft8/b16 -readout"); psk<vd::SOFT8, vd::B16, 8>(v, "ps soft8/b16 -tabbuild");
     psk<vd::SOFT8, vd::B16, 16>(v, "ps soft8/b16 -loads"); psk<vd::SOFT8, vd::B16, 256>(v, "ps soft8/b16 -fairness");
     psk<vd::SOFT8, vd::B16, 1 | 2 | 4 | 8 | 16>(v, "ps soft8/b16 ACS only");
+    psk<vd::HARD, vd::B32, 1 | 2 | 4 | 8 | 16>(v, "ps hard/b32 ACS only");
     // balanced grids (every SIMD the same waves): 6144 chunks; the rate is per 6144-chunk launch
     v.push_back({"tg soft8/b16 6144 chunks", (KFn)vd::vd_decode_tg<vd::SOFT8, vd::B16, 32, 0>, 1536});
     v.push_back({"ps soft8/b16 6144 chunks", (KFn)vd::vd_decode_ps<vd::SOFT8, vd::B16, 32, 0>, 768});
@@ -69,6 +71,11 @@ int main(int argc, char** argv)
     tgb<524288>(v, "tg hard/b32 pkfma+maxdpp"); tgs<524288>(v, "tg soft8/b16 pkfma+maxdpp");
     tgb<(1 << 20)>(v, "tg hard/b32 board sc1 loads"); tgs<(1 << 20)>(v, "tg soft8/b16 board sc1 loads");
     tgb<(1 << 21)>(v, "tg hard/b32 dpp no inner nop"); tgs<(1 << 21)>(v, "tg soft8/b16 dpp no inner nop");
+    tgs<8192>(v, "tg soft8/b16 q5 permlane"); tgs<16384>(v, "tg soft8/b16 q4 permlane16");
+    tgs<8192 | 16384>(v, "tg soft8/b16 q5 perm32 q4 perm16");
+    tgb<8192>(v, "tg hard/b32 q5 bpermute"); tgf<8192>(v, "tg fp32/f16 q5 permlane");
+    tgb<8192 | 1>(v, "tg hard/b32 bp5 -traceback"); tgb<8192 | 2>(v, "tg hard/b32 bp5 -tabreads"); tgb<8192 | 4>(v, "tg hard/b32 bp5 -readout");
+    tgb<8192 | 8>(v, "tg hard/b32 bp5 -tabbuild"); tgb<8192 | 16>(v, "tg hard/b32 bp5 -loads"); tgb<8192 | 256>(v, "tg hard/b32 bp5 -fairness"); tgb<2 | 4 | 8 | 16 | 1 | 8192>(v, "tg hard/b32 ACS only q5 bpermute"); tgs<2 | 4 | 8 | 16 | 1 | 8192>(v, "tg soft8/b16 ACS only q5 permlane");
     // variants that must decode exactly like the full kernel: outputs compared word for word below
     auto twin = [&](const char* a, const char* b) {
         int ia = -1, ib = -1;
@@ -78,10 +85,30 @@ int main(int argc, char** argv)
     twin("tg soft16/b32 full", "tg soft16/b32 fp32 max"); twin("tg soft16/b32 full", "tg soft16/b32 dpp three-op");
     twin("tg hard/b32 full", "ps hard/b32 full"); twin("tg soft8/b16 full", "ps soft8/b16 full");
     twin("tg soft16/b32 full", "ps soft16/b32 full"); twin("tg fp32/f16 full", "ps fp32/f16 full");
-    for (const char* k : {"sub+add+maxdpp", "pkfma+maxdpp", "board sc1 loads", "dpp no inner nop"}) {
+    for (const char* k : {"sub+add+maxdpp", "pkfma+maxdpp", "board sc1 loads", "dpp no inner nop", "q5 bpermute", "q5 permlane", "q4 permlane16",
+                          "q5 perm32 q4 perm16"}) {
         char a[96], b[96];
         snprintf(a, sizeof a, "tg hard/b32 full"); snprintf(b, sizeof b, "tg hard/b32 %s", k); twin(a, b);
         snprintf(a, sizeof a, "tg soft8/b16 full"); snprintf(b, sizeof b, "tg soft8/b16 %s", k); twin(a, b);
+    }
+    // optional filter (argv[2]): comma-separated name substrings; a kept variant keeps its exact twin
+    if (argc > 2) {
+        std::vector<int> keep(v.size(), 0);
+        std::string f = argv[2];
+        for (size_t i = 0; i < v.size(); i++) {
+            size_t a = 0;
+            while (a <= f.size()) {
+                size_t b = f.find(',', a); if (b == std::string::npos) b = f.size();
+                const std::string k = f.substr(a, b - a);
+                if (!k.empty() && strstr(v[i].name, k.c_str())) keep[i] = 1;
+                a = b + 1;
+            }
+        }
+        for (size_t i = 0; i < v.size(); i++) if (keep[i] && v[i].ref >= 0) keep[v[i].ref] = 1;
+        std::vector<Var> w; std::vector<int> idx(v.size(), -1);
+        for (size_t i = 0; i < v.size(); i++) if (keep[i]) { idx[i] = (int)w.size(); w.push_back(v[i]); }
+        for (auto& x : w) if (x.ref >= 0) x.ref = idx[x.ref];
+        v.swap(w);
     }
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
@@ -120,6 +147,7 @@ int main(int argc, char** argv)
         }
     }
     // per-wave clock stamps of the full kernel (ABL 32), without and with the priority schedule (64)
+    if (argc <= 2)  // not with a filter
     for (KFn f : {(KFn)vd::vd_decode_sc<vd::HARD, vd::B32, 32, 32>, (KFn)vd::vd_decode_tg<vd::HARD, vd::B32, 32, 32>}) {
         printf("=== %s\n", f == (KFn)vd::vd_decode_sc<vd::HARD, vd::B32, 32, 32> ? "sc full" : "tg full");
         for (int r = 0; r < 3; r++) hipLaunchKernelGGL(f, dim3(1600), dim3(256), 0, 0, in, out, g);

@@ -1,0 +1,105 @@
+// vd_benchab.hip -- timing-only A/B of kernel variants under bench conditions (not part of the product):
+// per step one 32M-bit HARD batch (int32 core) and one 32M-bit SOFT8 batch (int16 core), split launches,
+// codeword data (HARD: K=7 codeword through a BSC, p = 0.04; SOFT8: BPSK codeword + Gaussian noise at
+// Eb/N0 2 dB, quantised like SoftDecisionPacker(SOFT8)), K steps back to back with the launches grouped
+// per workload as bench.py does.  Variants alternate step group by step group, so clock and thermal drift
+// hit both alike.  Usage: vd_benchab [groups] [steps per group] [BSC p] [noise scale]
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstdlib>
+#include <cmath>
+#include <random>
+#include <vector>
+#include <algorithm>
+#include "../gpu-accelerated-viterbi-decoder_amd/csrc/vd_kernel_tg.h"
+#define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP error %s at %d\n", hipGetErrorString(e), __LINE__); exit(1); } } while (0)
+using KFn = void (*)(const void*, void*, vd::Geom);
+
+struct Variant { const char* name; KFn hard, soft8; };
+
+int main(int argc, char** argv)
+{
+    const int groups = argc > 1 ? atoi(argv[1]) : 8, steps = argc > 2 ? atoi(argv[2]) : 10;
+    const double pflip = argc > 3 ? atof(argv[3]) : 0.04, nscale = argc > 4 ? atof(argv[4]) : 1.0;
+    const size_t N = 32000000;  // coded stages per batch (the bench's 32M-bit input: 16M stages x 2)
+    const size_t stages = N / 2 * 2;
+    (void)stages;
+    // codeword
+    std::mt19937 rng(7);
+    std::vector<uint8_t> o0(N), o1(N);
+    uint32_t reg = 0;
+    for (size_t t = 0; t < N; t++) {
+        reg = ((reg >> 1) | ((rng() & 1u) << 6)) & 127u;
+        o0[t] = __builtin_popcount(reg & 0171u) & 1u;
+        o1[t] = __builtin_popcount(reg & 0133u) & 1u;
+    }
+    // HARD: BSC p = 0.04, 16 stages per word, MSB first
+    std::vector<uint32_t> hh(N / 16 + 64, 0u);
+    std::uniform_real_distribution<double> U(0.0, 1.0);
+    for (size_t t = 0; t < N; t++) {
+        uint32_t a = o0[t] ^ (U(rng) < pflip), b = o1[t] ^ (U(rng) < pflip);
+        hh[t / 16] |= (a << (31 - 2 * (t % 16))) | (b << (30 - 2 * (t % 16)));
+    }
+    // SOFT8: BPSK (bit 0 -> +1), rate 1/2 at Eb/N0 2 dB, scaled by 40000 / 2^8 and clamped like the packer's
+    // 8-bit code; 2 stages per word, stage g in the 16-bit half g ^ 1: s0 high byte, s1 low byte
+    const double sigma = nscale * std::sqrt(1.0 / (2.0 * 0.5 * std::pow(10.0, 0.2)));
+    std::normal_distribution<double> G(0.0, sigma);
+    auto q8 = [&](double x) { long v = std::lround(x * 40.0); v = std::min(127L, std::max(-128L, v)); return (uint32_t)(uint8_t)(int8_t)v; };
+    std::vector<uint32_t> hs(N / 2 + 64, 0u);
+    for (size_t t = 0; t < N; t++) {
+        const uint32_t s0 = q8((o0[t] ? -1.0 : 1.0) + G(rng)), s1 = q8((o1[t] ? -1.0 : 1.0) + G(rng));
+        const uint32_t half = (s0 << 8) | s1;
+        hs[t / 2] |= half << (16 * ((t % 2) ^ 1));
+    }
+    void *inH, *inS, *out;
+    CK(hipMalloc(&inH, hh.size() * 4));
+    CK(hipMalloc(&inS, hs.size() * 4));
+    CK(hipMalloc(&out, 16u << 20));
+    CK(hipMemcpy(inH, hh.data(), hh.size() * 4, hipMemcpyHostToDevice));
+    CK(hipMemcpy(inS, hs.data(), hs.size() * 4, hipMemcpyHostToDevice));
+    vd::Geom g;
+    g.packNum = (N - 64) / 32;
+    g.nchunks = 6400;
+    g.availStages = N;
+    g.scale = 1.0f;
+    CK(hipMalloc(&g.fair, vd::kFairBoardWords * 4));
+    CK(hipMemset(g.fair, 0xFF, vd::kFairBoardWords * 4));
+    float* spec; uint32_t* stats;
+    CK(hipMalloc(&spec, 256 * vd::kSplitVecs * 64 * 4));
+    CK(hipMalloc(&stats, 4));
+    CK(hipMemset(stats, 0, 4));
+    g.nwhole = 6144; g.spec = spec; g.stats = stats;
+    const Variant vs[] = {
+        {"product (hard permlane, soft8 bpermute)", (KFn)vd::vd_decode_tg<vd::HARD, vd::B32, 32, 0>, (KFn)vd::vd_decode_tg<vd::SOFT8, vd::B16, 32, 0>},
+        {"flipped (hard bpermute, soft8 permlane)", (KFn)vd::vd_decode_tg<vd::HARD, vd::B32, 32, 8192>, (KFn)vd::vd_decode_tg<vd::SOFT8, vd::B16, 32, 8192>},
+    };
+    const int nv = sizeof(vs) / sizeof(vs[0]);
+    hipEvent_t ev[3];
+    for (int i = 0; i < 3; i++) CK(hipEventCreate(&ev[i]));
+    std::vector<std::vector<float>> th(nv), ts(nv);
+    for (int r = 0; r < groups + 1; r++)
+        for (int v = 0; v < nv; v++) {
+            CK(hipEventRecord(ev[0]));
+            for (int k = 0; k < steps; k++) hipLaunchKernelGGL(vs[v].hard, dim3(1792), dim3(256), 0, 0, inH, out, g);
+            CK(hipEventRecord(ev[1]));
+            for (int k = 0; k < steps; k++) hipLaunchKernelGGL(vs[v].soft8, dim3(1792), dim3(256), 0, 0, inS, out, g);
+            CK(hipEventRecord(ev[2]));
+            CK(hipEventSynchronize(ev[2]));
+            float a, b;
+            CK(hipEventElapsedTime(&a, ev[0], ev[1]));
+            CK(hipEventElapsedTime(&b, ev[1], ev[2]));
+            if (r) { th[v].push_back(a / steps); ts[v].push_back(b / steps); }
+        }
+    uint32_t redec = 0;
+    CK(hipMemcpy(&redec, stats, 4, hipMemcpyDeviceToHost));
+    printf("%d groups x %d steps, BSC p %.3f, noise x %.2f, split launches, re-decoded split chunks: %u\n", groups, steps,
+           pflip, nscale, redec);
+    for (int v = 0; v < nv; v++) {
+        std::sort(th[v].begin(), th[v].end());
+        std::sort(ts[v].begin(), ts[v].end());
+        const double mh = th[v][th[v].size() / 2], ms = ts[v][ts[v].size() / 2];
+        printf("%-42s hard %.4f ms  soft8 %.4f ms  step %.4f ms -> %.1f Gb/s (soft8 %.1f)\n", vs[v].name, mh, ms, mh + ms,
+               2.0 * (double)(g.packNum * 32) / ((mh + ms) * 1e-3) / 1e9, (double)(g.packNum * 32) / (ms * 1e-3) / 1e9);
+    }
+    return 0;
+}

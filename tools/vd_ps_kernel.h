@@ -1,4 +1,11 @@
-// vd_kernel_ps.h -- "paired-state" decode kernel vd_decode_ps (gfx950): the tagged-metric scheme of
+// vd_ps_kernel.h -- TOOLS ONLY (timing studies, not in the product).  Round-2 experiment, kept for
+// tools/vd_ablate: exact (all GPU parity tests passed with it as the product kernel), but no faster than
+// vd_decode_tg in the bench (tg 150.1 / 151.0 Gb/s vs ps 150.0 / 150.2, interleaved, profiles/r02) and
+// slower per chunk (balanced 6144-chunk launch 0.1872 vs 0.1841 ms): at 3 waves per SIMD its LDS round
+// trips (swizzle, table reads) are exposed.  vd_decode_tg with the xor-32 exchange through ds_bpermute
+// took its place.
+//
+// "paired-state" decode kernel vd_decode_ps (gfx950): the tagged-metric scheme of
 // vd_kernel_tg.h (decisions in the low bits of an exact-integer fp32 / int32 metric, bit-field read-out,
 // group traceback) with TWO trellis states per lane and two chunks per wave.  Same decode semantics
 // (reference src/viterbi/viterbi.cu:144-207, viterbiACS.cuh:113-157,216-256, viterbiTB.cuh:4-21),
@@ -20,7 +27,7 @@
 // vd_kernel_tg.h: same check-and-re-decode protocol, kPsSlots pieces).  LDS per workgroup: 8 x (1,920 +
 // 12 x 256) = 39,936 B, so 4 workgroups (16 waves, 32 chunks) fit a CU: 6400 chunks = 25 per CU resident.
 #pragma once
-#include "vd_kernel_tg.h"
+#include "../gpu-accelerated-viterbi-decoder_amd/csrc/vd_kernel_tg.h"
 
 namespace vd {
 

@@ -91,6 +91,21 @@ int main(int argc, char** argv)
                simdEnd[simdEnd.size() / 2], simdEnd[simdEnd.size() * 9 / 10], simdEnd.back());
         for (auto& kv : endByCount) { auto v = kv.second; std::sort(v.begin(), v.end());
             printf("    SIMDs with %d waves: %zu, end med %.1f max %.1f\n", kv.first, v.size(), v[v.size() / 2], v.back()); }
+        {   // start skew and clock: wave start times, per-XCD median end and clock (s_memtime / s_memrealtime)
+            std::vector<double> st; std::map<uint32_t, std::vector<double>> xend, xmhz;
+            for (int w = 0; w < nw; w++) {
+                if (d[6 * w + 2] == 0) continue;
+                st.push_back((d[6 * w + 2] - r0) / 100.0);
+                const uint32_t xc = (uint32_t)d[6 * w + 5] & 7;
+                xend[xc].push_back((d[6 * w + 3] - r0) / 100.0);
+                xmhz[xc].push_back((double)(d[6 * w + 1] - d[6 * w]) / (double)(d[6 * w + 3] - d[6 * w + 2]) * 100.0);
+            }
+            std::sort(st.begin(), st.end());
+            printf("    wave start us: min %.1f p10 %.1f med %.1f p90 %.1f max %.1f\n", st[0], st[st.size() / 10], st[st.size() / 2],
+                   st[st.size() * 9 / 10], st.back());
+            for (auto& kv : xend) { auto a = kv.second, b = xmhz[kv.first]; std::sort(a.begin(), a.end()); std::sort(b.begin(), b.end());
+                printf("    XCD %u: wave end med %.1f max %.1f, clock med %.0f MHz\n", kv.first, a[a.size() / 2], a.back(), b[b.size() / 2]); }
+        }
         if (s) { printf("    piece waves per SIMD:"); for (auto& kv : pieceHist) printf(" %d:%d", kv.first, kv.second); printf("\n");
             std::vector<double> pe; for (int w = 6144; w < nw; w++) pe.push_back((d[6 * w + 3] - r0) / 100.0);
             std::sort(pe.begin(), pe.end()); printf("    piece wave end us: min %.1f med %.1f max %.1f\n", pe[0], pe[pe.size() / 2], pe.back()); }
