@@ -128,15 +128,18 @@ def acs_only_ms(name):
 
 def valu_view(pmc, kernel_ms, stages, name, msg_bits):
     """The bound that binds: VALU issue.  From the committed PMC summary of this kernel
-    (counters per dispatch, summed over the chip) and the live kernel time:
-      clock        = GRBM_GUI_ACTIVE / 8 XCDs / kernel time            (measured engine clock)
-      busy_pct     = 100 * SQ_ACTIVE_INST_VALU * 4 / (1024 SIMDs * GRBM_GUI_ACTIVE / 8)
+    (counters per dispatch, summed over the chip; the GRBM pass also ran --kernel-trace, so its kernel
+    time and clock come from the same dispatches):
+      cycles       = GRBM_GUI_ACTIVE / 8 XCDs                        (engine cycles of one dispatch)
+      clock        = cycles / that run's kernel time
+      busy_pct     = 100 * SQ_ACTIVE_INST_VALU * 4 / (1024 SIMDs * cycles)
                      (the gfx94x VALUBusy formula rocprofv3 falls back to on gfx950; it charges 4 cycles
                      per wave64 VALU instruction, a SIMD-16 model, so it reads above 100 on the 32-lane
                      gfx950 SIMD when every SIMD issues VALU back to back)
-      issue_pct    = 100 * SQ_INSTS_VALU * 2 / (1024 * GRBM_GUI_ACTIVE / 8)
+      issue_pct    = 100 * SQ_INSTS_VALU * 2 / (1024 * cycles)
                      (SIMD-32 model: a wave64 VALU instruction occupies its SIMD for 2 cycles at the
-                     least; max/DPP/permlane/bit-field forms take 4 -- profiles/r01/ubench_maxcost.log)
+                     least; max/DPP/permlane/bit-field forms take 4 -- profiles/r02/ubench12.log)
+      issue_pct_live = the same with the live kernel time at the PMC run's clock
       mix ceiling  = the same launch with only the ACS recursion (tools/vd_ablate)."""
     c = pmc.get("counters_mean_per_dispatch", {})
     if not c or "SQ_INSTS_VALU" not in c:
@@ -144,13 +147,19 @@ def valu_view(pmc, kernel_ms, stages, name, msg_bits):
     insts = c["SQ_INSTS_VALU"]
     v = {"insts_per_launch": round(insts), "insts_per_wave_stage": round(insts / stages, 3),
          "wave_stages_per_launch": stages}
+    if "SQ_INSTS_LDS" in c:
+        v["lds_insts_per_wave_stage"] = round(c["SQ_INSTS_LDS"] / stages, 3)
     if "GRBM_GUI_ACTIVE" in c:
         cyc = c["GRBM_GUI_ACTIVE"] / N_XCD
-        v["clock_ghz"] = round(cyc / (kernel_ms * 1e-3) / 1e9, 3)
         v["issue_pct"] = round(100.0 * insts * 2 / (N_SIMD * cyc), 1)
         if "SQ_ACTIVE_INST_VALU" in c:
             v["busy_pct"] = round(100.0 * c["SQ_ACTIVE_INST_VALU"] * 4 / (N_SIMD * cyc), 1)
         v["cycles_per_inst_per_simd"] = round(N_SIMD * cyc / insts, 3)
+        ghz = pmc.get("pmc_run_clock_ghz")
+        if ghz:
+            v["pmc_run_clock_ghz"] = round(ghz, 3)
+            v["pmc_run_kernel_ms"] = round(pmc["pmc_run_kernel_ns_median"] * 1e-6, 4)
+            v["issue_pct_live"] = round(100.0 * insts * 2 / (N_SIMD * kernel_ms * 1e-3 * ghz * 1e9), 1)
     acs = acs_only_ms(name)
     if acs:
         v["mix_ceiling"] = {"acs_only_ms": acs, "gbps": round(msg_bits / (acs * 1e-3) / 1e9, 2),
@@ -410,6 +419,8 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--warm-s", type=float, default=WARM_S,
+                    help="minimum warm-up in seconds of steps (GPU clock ramp; 0 for counter-collection runs)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-llr", action="store_true", help="skip the float-input (packer fused) side measurement")
     ap.add_argument("--no-pcie", action="store_true", help="skip the host-to-host pipelined side measurement")
@@ -478,7 +489,7 @@ def main():
     # ~17 % slow kernels (0.221 vs 0.186 ms HARD, profiles/r02/clock_ramp.log).
     nwarm = 0
     tw = time.perf_counter()
-    while nwarm < args.warmup or time.perf_counter() - tw < WARM_S:
+    while nwarm < args.warmup or time.perf_counter() - tw < args.warm_s:
         for b in batches:
             run(b)
         nwarm += 1

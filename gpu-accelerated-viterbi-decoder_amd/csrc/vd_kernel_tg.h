@@ -646,7 +646,7 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(7))
     // ahead; one ds_read_b64 at an even period also carries the entry of the stage 6 later.  The
     // loads are volatile LDS-address-space loads so they stay single ds_read_b64s (2 LDS cycles) in
     // program order -- left alone the compiler merges neighbours into ds_read2_b64 (8 cycles).
-    constexpr int TGD = 4;
+    constexpr int TGD = 4;  // 6 or 8 measured the same (profiles/r02/ablate_prefetch.log)
     typedef __attribute__((address_space(3))) const volatile f2v* lptr;
     const __attribute__((address_space(3))) char* tl = (const __attribute__((address_space(3))) char*)tabb;
     f2v vp[96];  // entry pair read for stage r (even period of a pair, or every M_B32 phase-0 stage)

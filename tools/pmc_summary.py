@@ -38,6 +38,14 @@ def main():
                 if k is None:
                     continue
                 vals[k][row["Counter_Name"]].append(float(row["Counter_Value"]))
+    # kernel durations of the passes run with --kernel-trace (the GRBM pass): the clock of that run
+    durs = defaultdict(list)
+    for f in glob.glob(os.path.join(root, "*", "*kernel_trace.csv")):
+        with open(f) as fh:
+            for row in csv.DictReader(fh):
+                k = short(row["Kernel_Name"])
+                if k is not None:
+                    durs[k].append(float(row["End_Timestamp"]) - float(row["Start_Timestamp"]))
     res = {}
     for k, cs in vals.items():
         m = {c: sum(v) / len(v) for c, v in cs.items()}
@@ -54,6 +62,11 @@ def main():
             r["valu_insts_per_wave"] = m["SQ_INSTS_VALU"] / m["SQ_WAVES"]
         if "SQ_INSTS_LDS" in m and "SQ_WAVES" in m:
             r["lds_insts_per_wave"] = m["SQ_INSTS_LDS"] / m.get("SQ_WAVES", 1)
+        if durs.get(k):
+            d = sorted(durs[k])
+            r["pmc_run_kernel_ns_median"] = d[len(d) // 2]
+            if "GRBM_GUI_ACTIVE" in m:  # summed over the 8 XCDs
+                r["pmc_run_clock_ghz"] = m["GRBM_GUI_ACTIVE"] / 8 / (sum(d) / len(d))
         res[k] = r
     with open(out, "w") as fh:
         json.dump(res, fh, indent=1, sort_keys=True)
