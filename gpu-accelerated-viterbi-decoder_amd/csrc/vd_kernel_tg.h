@@ -188,6 +188,15 @@ __device__ __forceinline__ float tg_partner(float V, int paddr)
 {
     return __builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute(paddr, __builtin_bit_cast(int, V)));
 }
+// M_B32 phase-0 stage with the signed entry (S32 in the kernel): V' = max(V + s*m, V_partner - s*m)
+template <int SEL>
+__device__ __forceinline__ void tg_stage_lds_sg(float& V, f2v e, float vp, float sg)
+{
+    const float m = SEL == 0 ? e.x : e.y;
+    float t1, t2;
+    asm("v_fma_f32 %1, %3, %5, %0\n\tv_fma_f32 %2, -%3, %5, %4\n\tv_max_f32 %0, %1, %2"
+        : "+{v60}"(V), "=&v"(t1), "=&v"(t2) : "v"(m), "v"(vp), "v"(sg));
+}
 template <int SEL>
 __device__ __forceinline__ void tg_stage_lds(float& V, f2v e, float vp, bool upper)
 {
@@ -537,15 +546,19 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(7))
     constexpr bool INT = TgFmt<CH>::INT;
     static_assert(!INT || CORE == B32, "int32 patterns: SOFT16 on the int32 core only");
     constexpr bool FM = INT && (ABL & (1 << 22));  // study: signed max on the patterns as fp32
-    using TT = TgTab<CORE>;
+    // xor-32 (Q=5) exchange: the partner's metric through the LDS crossbar (ds_bpermute, then three
+    // plain VALU ops) instead of v_permlane32_swap (pk_fma, swap, max).  ABL 8192 (tools): the swap.
+    constexpr bool BP5 = !INT && !(ABL & 8192);
+    // M_B32 with the LDS exchange (S32): its phase-0 tie rule differs between the position halves (upper
+    // half: own wins, tag +2^j).  Instead of rows holding both tag signs, the upper lanes read the entry of
+    // the complementary label in the ordinary row (tag -2^j) and negate it: BM[3-L] = -BM[L], so
+    // -(BM[3-L]*2^S - 2^j) = BM[L]*2^S + 2^j.  The stage then forms V + s*e and V_partner - s*e with
+    // s = -1 in the upper half (v_fma, as cheap as v_add): the same values as before, and the M_B32 table
+    // becomes the M_B16 one (no pair rows: fewer LDS reads and writes).
+    constexpr bool S32 = CORE == B32 && BP5;
+    using TT = TgTab<S32 ? B16 : CORE>;
     constexpr int J = TgFmt<CH>::J, S = TgFmt<CH>::S;
     constexpr int TBS = TgRing<CORE>::TBS;
-    // xor-32 (Q=5) exchange: the partner's metric through the LDS crossbar (ds_bpermute, then the DPP
-    // stage's three ops) on the B16 / F16 cores, v_permlane32_swap (pk_fma, swap, max) on M_B32, whose
-    // heavier LDS load (pair rows: more table reads and writes) turns the extra LDS round trip into a
-    // loss (tools/vd_ablate, profiles/r02/ablate_q5.log: SOFT8/B16 -5 %, HARD/B32 +4.5 %).  ABL 8192
-    // (tools) flips the choice.
-    constexpr bool BP5 = !INT && ((CORE == B32) == ((ABL & 8192) != 0));
     __shared__ __attribute__((aligned(16))) char tab_all[kWaves][TT::BYTES];
     __shared__ __attribute__((aligned(256))) uint32_t ring_all[kWaves][(TBS + 1) * 64];  // bit 31-s = stage s
     const int lane = threadIdx.x & 63;
@@ -575,6 +588,8 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(7))
         constexpr int K = decltype(KK)::value;
         aK[K] = 8 * own_label(pos, K);
     });
+    if constexpr (S32) aK[0] = upper5 ? 24 - aK[0] : aK[0];  // upper half: the complementary label 3 - L
+    const float sg0 = upper5 ? -1.0f : 1.0f;                  // S32: sign of the phase-0 entry
     // INT phase-0 swap stage: this lane's signed pair, read as two dwords of the (E-, E+) pair row:
     // (E-[L], -E+[L]) = (E-[L], E-[3-L]) in the lower position half, (-E-[L], E+[L]) = (E+[3-L], E+[L]) in
     // the upper one (BM[3-L] = -BM[L])
@@ -712,6 +727,10 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(7))
                 // ABL 1<<21 (study): no s_nop inside the stage where hipcc pads the asm boundary itself
                 constexpr bool NOPD = !(ABL & (1 << 21)) || i % 16 == 0;
                 tg_stage_dpp<DCTRL, NOPD>(V, m);
+            } else if constexpr (LSW && S32 && IS32) {
+                const float pv = tg_partner(V, pa5);
+                const f2v e = (ABL & 2) ? (f2v){(float)aK[K], 1.0f} : vp[RP];
+                tg_stage_lds_sg<ODD ? 1 : 0>(V, e, pv, sg0);
             } else if constexpr (LSW) {
                 const float pv = IS16 ? __builtin_bit_cast(float, __builtin_amdgcn_ds_swizzle(__builtin_bit_cast(int, V), 0x401F))
                                       : tg_partner(V, pa5);
@@ -812,7 +831,7 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(7))
         e[2] = E1;
         e[4] = E2;
         e[6] = E3;
-        if constexpr (CORE == B32) {
+        if constexpr (TT::pairrow(0)) {  // M_B32 with the lane swap: phase-0 rows hold both tag signs
             if (K == 0) {
                 e[1] = __builtin_fmaf(af, -SC, tagv);
                 e[3] = __builtin_fmaf(bf, -SC, tagv);

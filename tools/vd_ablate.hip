@@ -73,9 +73,9 @@ int main(int argc, char** argv)
     tgb<(1 << 21)>(v, "tg hard/b32 dpp no inner nop"); tgs<(1 << 21)>(v, "tg soft8/b16 dpp no inner nop");
     tgs<8192>(v, "tg soft8/b16 q5 permlane"); tgs<16384>(v, "tg soft8/b16 q4 permlane16");
     tgs<8192 | 16384>(v, "tg soft8/b16 q5 perm32 q4 perm16");
-    tgb<8192>(v, "tg hard/b32 q5 bpermute"); tgf<8192>(v, "tg fp32/f16 q5 permlane");
-    tgb<8192 | 1>(v, "tg hard/b32 bp5 -traceback"); tgb<8192 | 2>(v, "tg hard/b32 bp5 -tabreads"); tgb<8192 | 4>(v, "tg hard/b32 bp5 -readout");
-    tgb<8192 | 8>(v, "tg hard/b32 bp5 -tabbuild"); tgb<8192 | 16>(v, "tg hard/b32 bp5 -loads"); tgb<8192 | 256>(v, "tg hard/b32 bp5 -fairness"); tgb<2 | 4 | 8 | 16 | 1 | 8192>(v, "tg hard/b32 ACS only q5 bpermute"); tgs<2 | 4 | 8 | 16 | 1 | 8192>(v, "tg soft8/b16 ACS only q5 permlane");
+    tgb<8192>(v, "tg hard/b32 q5 permlane"); tgf<8192>(v, "tg fp32/f16 q5 permlane");
+    tgb<8192 | 1>(v, "tg hard/b32 perm32 -traceback"); tgb<8192 | 2>(v, "tg hard/b32 perm32 -tabreads"); tgb<8192 | 4>(v, "tg hard/b32 perm32 -readout");
+    tgb<8192 | 8>(v, "tg hard/b32 perm32 -tabbuild"); tgb<8192 | 16>(v, "tg hard/b32 perm32 -loads"); tgb<8192 | 256>(v, "tg hard/b32 perm32 -fairness"); tgb<2 | 4 | 8 | 16 | 1 | 8192>(v, "tg hard/b32 ACS only q5 permlane"); tgs<2 | 4 | 8 | 16 | 1 | 8192>(v, "tg soft8/b16 ACS only q5 permlane");
     // variants that must decode exactly like the full kernel: outputs compared word for word below
     auto twin = [&](const char* a, const char* b) {
         int ia = -1, ib = -1;

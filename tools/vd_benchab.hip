@@ -70,8 +70,8 @@ int main(int argc, char** argv)
     CK(hipMemset(stats, 0, 4));
     g.nwhole = 6144; g.spec = spec; g.stats = stats;
     const Variant vs[] = {
-        {"product (hard permlane, soft8 bpermute)", (KFn)vd::vd_decode_tg<vd::HARD, vd::B32, 32, 0>, (KFn)vd::vd_decode_tg<vd::SOFT8, vd::B16, 32, 0>},
-        {"flipped (hard bpermute, soft8 permlane)", (KFn)vd::vd_decode_tg<vd::HARD, vd::B32, 32, 8192>, (KFn)vd::vd_decode_tg<vd::SOFT8, vd::B16, 32, 8192>},
+        {"product (xor-32 by ds_bpermute)", (KFn)vd::vd_decode_tg<vd::HARD, vd::B32, 32, 0>, (KFn)vd::vd_decode_tg<vd::SOFT8, vd::B16, 32, 0>},
+        {"xor-32 by v_permlane32_swap", (KFn)vd::vd_decode_tg<vd::HARD, vd::B32, 32, 8192>, (KFn)vd::vd_decode_tg<vd::SOFT8, vd::B16, 32, 8192>},
         {"DPP stages pk_fma + max_dpp (2 ops)", (KFn)vd::vd_decode_tg<vd::HARD, vd::B32, 32, 524288>, (KFn)vd::vd_decode_tg<vd::SOFT8, vd::B16, 32, 524288>},
         {"DPP stages sub + add + max_dpp", (KFn)vd::vd_decode_tg<vd::HARD, vd::B32, 32, 262144>, (KFn)vd::vd_decode_tg<vd::SOFT8, vd::B16, 32, 262144>},
     };
