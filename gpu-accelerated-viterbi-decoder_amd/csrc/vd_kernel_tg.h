@@ -556,6 +556,10 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(7))
     // s = -1 in the upper half (v_fma, as cheap as v_add): the same values as before, and the M_B32 table
     // becomes the M_B16 one (no pair rows: fewer LDS reads and writes).
     constexpr bool S32 = CORE == B32 && BP5;
+    // DPP stages as v_sub, v_add, v_max_f32_dpp (the partner's V - m through the DPP operand) instead of
+    // v_add, v_sub_f32_dpp, v_max: the same decisions; 1 % faster on M_B32 under bench conditions, no
+    // difference elsewhere (profiles/r02/benchab_*.log).  ABL 262144 (tools) flips the choice.
+    constexpr bool DPP2 = (CORE == B32) != ((ABL & 262144) != 0);
     using TT = TgTab<S32 ? B16 : CORE>;
     constexpr int J = TgFmt<CH>::J, S = TgFmt<CH>::S;
     constexpr int TBS = TgRing<CORE>::TBS;
@@ -718,8 +722,8 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(7))
                     const float pv = __builtin_bit_cast(float, __builtin_amdgcn_ds_swizzle(__builtin_bit_cast(int, V), 0x401F));
                     tg_stage_lds_i<FM>(V, ODD ? vp[RP].y : vp[RP].x, pv);
                 }
-            } else if constexpr (((!IS16 && !IS32) || (ABL & 128)) && (ABL & (262144 | 524288)) && !TT::pairrow(K)) {
-                // ABL (tools only): 262144 = sub, add, max_dpp; 524288 = pk_fma, max_dpp
+            } else if constexpr (((!IS16 && !IS32) || (ABL & 128)) && (DPP2 || (ABL & 524288)) && !TT::pairrow(K)) {
+                // two-op DPP forms: sub, add, max_dpp (DPP2); ABL 524288 (tools) pk_fma, max_dpp
                 const f2v e = (ABL & 2) ? (f2v){(float)aK[K], 1.0f} : vp[RP];
                 tg_stage_dpp2<DCTRL, ODD ? 1 : 0, (ABL & 524288) != 0>(V, e, spm);
             } else if constexpr ((!IS16 && !IS32) || (ABL & 128)) {

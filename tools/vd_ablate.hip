@@ -67,7 +67,7 @@ int main(int argc, char** argv)
     v.push_back({"tg soft8/b16 6144 chunks", (KFn)vd::vd_decode_tg<vd::SOFT8, vd::B16, 32, 0>, 1536});
     v.push_back({"ps soft8/b16 6144 chunks", (KFn)vd::vd_decode_ps<vd::SOFT8, vd::B16, 32, 0>, 768});
     tgs<0>(v, "tg soft8/b16 full"); tgs<1>(v, "tg soft8/b16 -traceback"); tgs<2>(v, "tg soft8/b16 -tabreads"); tgs<4>(v, "tg soft8/b16 -readout"); tgf<0>(v, "tg fp32/f16 full");
-    tgb<262144>(v, "tg hard/b32 sub+add+maxdpp"); tgs<262144>(v, "tg soft8/b16 sub+add+maxdpp");
+    tgb<262144>(v, "tg hard/b32 add+subdpp+max"); tgs<262144>(v, "tg soft8/b16 sub+add+maxdpp");
     tgb<524288>(v, "tg hard/b32 pkfma+maxdpp"); tgs<524288>(v, "tg soft8/b16 pkfma+maxdpp");
     tgb<(1 << 20)>(v, "tg hard/b32 board sc1 loads"); tgs<(1 << 20)>(v, "tg soft8/b16 board sc1 loads");
     tgb<(1 << 21)>(v, "tg hard/b32 dpp no inner nop"); tgs<(1 << 21)>(v, "tg soft8/b16 dpp no inner nop");
@@ -85,7 +85,7 @@ int main(int argc, char** argv)
     twin("tg soft16/b32 full", "tg soft16/b32 fp32 max"); twin("tg soft16/b32 full", "tg soft16/b32 dpp three-op");
     twin("tg hard/b32 full", "ps hard/b32 full"); twin("tg soft8/b16 full", "ps soft8/b16 full");
     twin("tg soft16/b32 full", "ps soft16/b32 full"); twin("tg fp32/f16 full", "ps fp32/f16 full");
-    for (const char* k : {"sub+add+maxdpp", "pkfma+maxdpp", "board sc1 loads", "dpp no inner nop", "q5 bpermute", "q5 permlane", "q4 permlane16",
+    for (const char* k : {"sub+add+maxdpp", "add+subdpp+max", "pkfma+maxdpp", "board sc1 loads", "dpp no inner nop", "q5 bpermute", "q5 permlane", "q4 permlane16",
                           "q5 perm32 q4 perm16"}) {
         char a[96], b[96];
         snprintf(a, sizeof a, "tg hard/b32 full"); snprintf(b, sizeof b, "tg hard/b32 %s", k); twin(a, b);
