@@ -1,0 +1,67 @@
+"""bench.py's contract (host logic on CPU, the JSON line on the GPU).
+
+CPU: the roofline helpers read the committed round profiles (profiles/<PMC_ROUND>/pmc_summary.json and
+ablate.log) the way the bench line quotes them.  GPU: a short bench run prints one JSON line with the keys
+the driver and the judge read (metric, value, roofline with its binding VALU view, config)."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import bench  # noqa: E402
+
+
+def test_algorithmic_bytes_match_survey():
+    # HARD 0.375 B, SOFT8 2.125 B per decoded bit at 32M bits (31,999,936 decoded bits)
+    n = 2 * bench.N_BITS
+    assert bench.algorithmic_bytes(0x00, n) == 11_999_992
+    assert bench.algorithmic_bytes(0x12, n) == 67_999_992
+
+
+def test_mix_ceiling_from_committed_ablation():
+    for name in ("hard_b32", "soft8_b16"):
+        ms = bench.acs_only_ms(name)
+        assert ms is not None and 0.05 < ms < 0.5, (name, ms)
+    assert bench.acs_only_ms("fp32_f16") is None
+
+
+def test_valu_view_from_committed_pmc():
+    pmc = bench.load_pmc()
+    assert {"hard_b32", "soft8_b16"} <= set(pmc)
+    for name in ("hard_b32", "soft8_b16"):
+        p = pmc[name]
+        # HBM bytes per launch within 1.2x of the algorithmic bytes
+        alg = bench.algorithmic_bytes(0x00 if name == "hard_b32" else 0x12, 2 * bench.N_BITS)
+        assert alg <= p["traffic_bytes"] <= 1.2 * alg, (name, p["traffic_bytes"], alg)
+        v = bench.valu_view(p, 0.18, 32_409_536, name, 31_999_936)
+        for k in ("insts_per_wave_stage", "issue_pct", "busy_pct", "cycles_per_inst_per_simd", "pmc_run_clock_ghz",
+                  "issue_pct_live", "mix_ceiling"):
+            assert k in v, (name, k)
+        assert 3.0 < v["insts_per_wave_stage"] < 5.0
+        assert 1.5 < v["pmc_run_clock_ghz"] < 2.6
+
+
+@pytest.mark.gpu
+def test_bench_prints_one_json_line_with_the_contract_keys():
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "3", "--warmup", "1", "--warm-s", "0.05",
+           "--no-cpu-baseline", "--no-llr", "--no-pcie", "--no-channel", "--no-other"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+              "vs_baseline", "dtype", "data", "config", "roofline"):
+        assert k in d, k
+    assert d["n_gpus"] == 1 and d["steps"] == 3 and d["unit"] == "Gb/s" and d["value"] > 0
+    ro = d["roofline"]
+    assert ro["bound"] == "valu" and ro["unit"] == "GB/s" and 0 < ro["frac"] < 1
+    assert ro["kernel"].startswith("soft8_b16")
+    assert {"hard_b32", "soft8_b16"} == set(ro["per_kernel"])
+    assert ro["int_op_roofline"]["ops_per_bit"] == 256
+    # both batches decoded correctly at the bench SNR (the harness chain is near noiseless there)
+    assert all(b < 1e-5 for b in d["config"]["ber"].values())
