@@ -81,13 +81,6 @@ __device__ __forceinline__ int tg_pos(int l)
     const int p2 = (l >> 2) & 1;
     return (l & ~7) | (p2 << 2) | ((((l >> 1) & 1) ^ p2) << 1) | ((l & 1) ^ p2);
 }
-// alternative map (ABL 131072, timing study): l = p0*1 ^ p1*2 ^ p4*7 ^ p3*8 ^ p2*16 ^ p5*32
-__device__ __forceinline__ int tg_pos_b(int l)
-{
-    const int p4 = (l >> 2) & 1;
-    return ((l & 1) ^ p4) | ((((l >> 1) & 1) ^ p4) << 1) | (((l >> 4) & 1) << 2) | (((l >> 3) & 1) << 3) | (p4 << 4) |
-           (((l >> 5) & 1) << 5);
-}
 // reference label (0..3) of position p's own predecessor branch at stage phase k, and its parity helper
 __host__ __device__ constexpr int tg_par7(int v) { return (v & 1) ^ ((v >> 1) & 1) ^ ((v >> 2) & 1) ^ ((v >> 3) & 1) ^ ((v >> 4) & 1) ^ ((v >> 5) & 1) ^ ((v >> 6) & 1); }
 __host__ __device__ constexpr int tg_label(int p, int k)
@@ -104,17 +97,12 @@ static_assert(tg_label(32, 0) == 0 && tg_label(16, 5) == 0, "swap partners share
 // name the pair v[60:61] and read V for both of its halves (op_sel_hi 0); v62:v63 are its scratch.
 typedef float f2v __attribute__((ext_vector_type(2)));
 // DPP stage, exchange lane xor {1,2,7,8}[Q].  The DPP source (V) is >= 2 VALU slots after its write.
-template <int Q, bool NOP = true>
+template <int Q>
 __device__ __forceinline__ void tg_stage_dpp(float& V, float m)
 {
     float t1, t2;
 #define VD_TG_DPP(CTRL)                                                                                   \
-    if constexpr (NOP)                                                                                    \
     asm("v_add_f32 %1, %0, %3\n\ts_nop 0\n\tv_sub_f32_dpp %2, %0, %3 " CTRL " row_mask:0xf bank_mask:0xf\n\t" \
-        "v_max_f32 %0, %1, %2"                                                                           \
-        : "+{v60}"(V), "=&v"(t1), "=&v"(t2) : "v"(m));                                                   \
-    else                                                                                                  \
-    asm("v_add_f32 %1, %0, %3\n\tv_sub_f32_dpp %2, %0, %3 " CTRL " row_mask:0xf bank_mask:0xf\n\t"      \
         "v_max_f32 %0, %1, %2"                                                                           \
         : "+{v60}"(V), "=&v"(t1), "=&v"(t2) : "v"(m))
     if constexpr (Q == 0) VD_TG_DPP("quad_perm:[1,0,3,2]");
@@ -123,62 +111,39 @@ __device__ __forceinline__ void tg_stage_dpp(float& V, float m)
     else VD_TG_DPP("row_ror:8");
 #undef VD_TG_DPP
 }
-// DPP stage, two ops: the butterfly partner has the same branch label in every phase (and, outside
-// M_B32's phase-0 swap rows, the same tag), so its V_exch - m is what this lane would compute from its own
-// V.  One v_pk_fma_f32 forms [a, b] = [V + m, V - m] in every lane, and the max takes b from the partner
-// through the DPP operand: V' = max(a, dpp(b)).  v_add/v_sub/v_fma issue in half the cycles of a DPP op
-// or a v_max (tools/vd_ubench11), so this beats add + sub_dpp + max.  b is read by DPP 2 slots after its
-// write (s_nop 1).  SEL as tg_stage_swap (0 = even period, 1 = odd period of the entry pair e).
-template <int Q, int SEL, bool PK>
-__device__ __forceinline__ void tg_stage_dpp2(float& V, f2v e, f2v s)
+// DPP stage, two-op form: the butterfly partner has the same branch label and tag in every DPP phase,
+// so its V_exch - m is what this lane would compute from its own V: a = V + m, b = V - m, and the max
+// takes b from the partner through the DPP operand, V' = max(a, dpp(b)).  b is read by DPP 2 slots
+// after its write.
+template <int Q>
+__device__ __forceinline__ void tg_stage_dpp2(float& V, float m)
 {
-    const float m = SEL == 0 ? e.x : e.y;
+    float a, b;
 #define VD_TG_DPP2(CTRL)                                                                                     \
-    if constexpr (PK) {                                                                                      \
-        if constexpr (SEL == 0)                                                                              \
-            asm("v_pk_fma_f32 v[62:63], %1, %2, v[60:61] op_sel:[0,0,0] op_sel_hi:[0,1,0]\n\ts_nop 1\n\t"     \
-                "v_max_f32_dpp %0, v63, v62 " CTRL " row_mask:0xf bank_mask:0xf"                               \
-                : "+{v60}"(V) : "v"(e), "v"(s) : "v62", "v63");                                              \
-        else                                                                                                 \
-            asm("v_pk_fma_f32 v[62:63], %1, %2, v[60:61] op_sel:[1,0,0] op_sel_hi:[1,1,0]\n\ts_nop 1\n\t"     \
-                "v_max_f32_dpp %0, v63, v62 " CTRL " row_mask:0xf bank_mask:0xf"                               \
-                : "+{v60}"(V) : "v"(e), "v"(s) : "v62", "v63");                                              \
-    } else {                                                                                                 \
-        float a, b;                                                                                          \
-        asm("v_sub_f32 %2, %0, %3\n\tv_add_f32 %1, %0, %3\n\ts_nop 0\n\t"                                  \
-            "v_max_f32_dpp %0, %2, %1 " CTRL " row_mask:0xf bank_mask:0xf"                                     \
-            : "+{v60}"(V), "=&v"(a), "=&v"(b) : "v"(m));                                                    \
-    }
-    if constexpr (Q == 0) { VD_TG_DPP2("quad_perm:[1,0,3,2]") }
-    else if constexpr (Q == 1) { VD_TG_DPP2("quad_perm:[2,3,0,1]") }
-    else if constexpr (Q == 2) { VD_TG_DPP2("row_half_mirror") }
-    else { VD_TG_DPP2("row_ror:8") }
+    asm("v_sub_f32 %2, %0, %3\n\tv_add_f32 %1, %0, %3\n\ts_nop 0\n\t"                                      \
+        "v_max_f32_dpp %0, %2, %1 " CTRL " row_mask:0xf bank_mask:0xf"                                         \
+        : "+{v60}"(V), "=&v"(a), "=&v"(b) : "v"(m))
+    if constexpr (Q == 0) VD_TG_DPP2("quad_perm:[1,0,3,2]");
+    else if constexpr (Q == 1) VD_TG_DPP2("quad_perm:[2,3,0,1]");
+    else if constexpr (Q == 2) VD_TG_DPP2("row_half_mirror");
+    else VD_TG_DPP2("row_ror:8");
 #undef VD_TG_DPP2
 }
-// swap stage, exchange lane xor 16 (Q=4) or 32 (Q=5): [a, b] = [m, m'] * [sx, -sx] + [V, V] in one
-// v_pk_fma_f32, swap halves across lanes, max.  The butterfly partner has the same label in both swap
-// phases, so m' = m except in M_B32's phase-0 rows (m, m' = the two tag signs).  SEL picks the halves of
-// the table pair e: 0 = (lo, lo) (even period), 1 = (hi, hi) (odd period), 2 = (lo, hi) (M_B32 phase 0).
-// VAR (tools only, timing studies; results wrong): 1 no lane swap, 2 s_nop 0, 4 swap + max only
-template <int Q, int SEL, int VAR = 0>
+// xor-32 swap stage (tools, ABL 8192): [a, b] = [m, m'] * [sx, -sx] + [V, V] in one v_pk_fma_f32, swap
+// halves across lanes, max.  The butterfly partner has the same label, so m' = m except in M_B32's
+// phase-0 rows (m, m' = the two tag signs).  SEL picks the halves of the table pair e: 0 = (lo, lo) (even
+// period), 1 = (hi, hi) (odd period), 2 = (lo, hi) (M_B32 phase 0).
+template <int SEL>
 __device__ __forceinline__ void tg_stage_swap(float& V, f2v e, f2v s)
 {
-#define VD_TG_ASM(PK, NOP, SWP) \
-    asm(PK NOP SWP "v_max_f32 %0, v62, v63" : "+{v60}"(V) : "v"(e), "v"(s) : "v62", "v63")
-#define VD_TG_SWAP(SW, OS)                                                                                  \
-    if constexpr (VAR == 0) VD_TG_ASM("v_pk_fma_f32 v[62:63], %1, %2, v[60:61] " OS "\n\t", "s_nop 1\n\t", SW " v62, v63\n\t"); \
-    else if constexpr (VAR == 1) VD_TG_ASM("v_pk_fma_f32 v[62:63], %1, %2, v[60:61] " OS "\n\t", "s_nop 1\n\t", "");              \
-    else if constexpr (VAR == 2) VD_TG_ASM("v_pk_fma_f32 v[62:63], %1, %2, v[60:61] " OS "\n\t", "s_nop 0\n\t", SW " v62, v63\n\t"); \
-    else VD_TG_ASM("", "s_nop 1\n\t", SW " v62, v63\n\t");
-#define VD_TG_SWAP_SEL(SW)                                                                                  \
-    if constexpr (SEL == 0) { VD_TG_SWAP(SW, "op_sel:[0,0,0] op_sel_hi:[0,1,0]") }                           \
-    else if constexpr (SEL == 1) { VD_TG_SWAP(SW, "op_sel:[1,0,0] op_sel_hi:[1,1,0]") }                      \
-    else { VD_TG_SWAP(SW, "op_sel:[0,0,0] op_sel_hi:[1,1,0]") }
-    if constexpr (Q == 4) { VD_TG_SWAP_SEL("v_permlane16_swap_b32") }
-    else { VD_TG_SWAP_SEL("v_permlane32_swap_b32") }
-#undef VD_TG_SWAP_SEL
+#define VD_TG_SWAP(OS)                                                                                      \
+    asm("v_pk_fma_f32 v[62:63], %1, %2, v[60:61] " OS "\n\ts_nop 1\n\tv_permlane32_swap_b32 v62, v63\n\t"      \
+        "v_max_f32 %0, v62, v63"                                                                           \
+        : "+{v60}"(V) : "v"(e), "v"(s) : "v62", "v63")
+    if constexpr (SEL == 0) VD_TG_SWAP("op_sel:[0,0,0] op_sel_hi:[0,1,0]");
+    else if constexpr (SEL == 1) VD_TG_SWAP("op_sel:[1,0,0] op_sel_hi:[1,1,0]");
+    else VD_TG_SWAP("op_sel:[0,0,0] op_sel_hi:[1,1,0]");
 #undef VD_TG_SWAP
-#undef VD_TG_ASM
 }
 
 // swap stage with the partner's metric fetched through the LDS crossbar (ds_bpermute, no memory access)
@@ -223,17 +188,12 @@ __device__ __forceinline__ void tg_stage_dpp_i2(float& V, float m)
     else VD_TG_DPPI2("row_ror:8");
 #undef VD_TG_DPPI2
 }
-// FM (study, ABL 1<<22): the max on the patterns as fp32 (patterns kept positive normal floats)
-template <int Q, bool FM = false>
+// three-op form (tools, ABL 1<<24)
+template <int Q>
 __device__ __forceinline__ void tg_stage_dpp_i(float& V, float m)
 {
     float t1, t2;
 #define VD_TG_DPPI(CTRL)                                                                                  \
-    if constexpr (FM)                                                                                     \
-    asm("v_add_u32 %1, %0, %3\n\ts_nop 0\n\tv_sub_u32_dpp %2, %0, %3 " CTRL " row_mask:0xf bank_mask:0xf\n\t" \
-        "v_max_f32 %0, %1, %2"                                                                           \
-        : "+{v60}"(V), "=&v"(t1), "=&v"(t2) : "v"(m));                                                   \
-    else                                                                                                  \
     asm("v_add_u32 %1, %0, %3\n\ts_nop 0\n\tv_sub_u32_dpp %2, %0, %3 " CTRL " row_mask:0xf bank_mask:0xf\n\t" \
         "v_max_i32 %0, %1, %2"                                                                           \
         : "+{v60}"(V), "=&v"(t1), "=&v"(t2) : "v"(m))
@@ -245,27 +205,16 @@ __device__ __forceinline__ void tg_stage_dpp_i(float& V, float m)
 }
 // xor-32 swap stage: e = this lane's signed pair, (E-, -E+) in the lower position half, (-E-, E+) in the
 // upper one, so both halves form [a, b] = [V + e.x, V + e.y] and swap as the fp32 stage does
-template <bool FM = false>
 __device__ __forceinline__ void tg_stage_swap_i(float& V, f2v e)
 {
-    if constexpr (FM)
-        asm("v_add_u32 v62, %0, %1\n\tv_add_u32 v63, %0, %2\n\ts_nop 1\n\tv_permlane32_swap_b32 v62, v63\n\t"
-            "v_max_f32 %0, v62, v63"
-            : "+{v60}"(V) : "v"(e.x), "v"(e.y) : "v62", "v63");
-    else
-        asm("v_add_u32 v62, %0, %1\n\tv_add_u32 v63, %0, %2\n\ts_nop 1\n\tv_permlane32_swap_b32 v62, v63\n\t"
+    asm("v_add_u32 v62, %0, %1\n\tv_add_u32 v63, %0, %2\n\ts_nop 1\n\tv_permlane32_swap_b32 v62, v63\n\t"
             "v_max_i32 %0, v62, v63"
             : "+{v60}"(V) : "v"(e.x), "v"(e.y) : "v62", "v63");
 }
-template <bool FM = false>
 __device__ __forceinline__ void tg_stage_lds_i(float& V, float m, float vp)
 {
     float t1, t2;
-    if constexpr (FM)
-        asm("v_add_u32 %1, %0, %3\n\tv_sub_u32 %2, %4, %3\n\tv_max_f32 %0, %1, %2"
-            : "+{v60}"(V), "=&v"(t1), "=&v"(t2) : "v"(m), "v"(vp));
-    else
-        asm("v_add_u32 %1, %0, %3\n\tv_sub_u32 %2, %4, %3\n\tv_max_i32 %0, %1, %2"
+    asm("v_add_u32 %1, %0, %3\n\tv_sub_u32 %2, %4, %3\n\tv_max_i32 %0, %1, %2"
             : "+{v60}"(V), "=&v"(t1), "=&v"(t2) : "v"(m), "v"(vp));
 }
 
@@ -545,7 +494,6 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(7))
     using IN = TgIn<CH>;
     constexpr bool INT = TgFmt<CH>::INT;
     static_assert(!INT || CORE == B32, "int32 patterns: SOFT16 on the int32 core only");
-    constexpr bool FM = INT && (ABL & (1 << 22));  // study: signed max on the patterns as fp32
     // xor-32 (Q=5) exchange: the partner's metric through the LDS crossbar (ds_bpermute, then three
     // plain VALU ops) instead of v_permlane32_swap (pk_fma, swap, max).  ABL 8192 (tools): the swap.
     constexpr bool BP5 = !INT && !(ABL & 8192);
@@ -567,8 +515,7 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(7))
     __shared__ __attribute__((aligned(256))) uint32_t ring_all[kWaves][(TBS + 1) * 64];  // bit 31-s = stage s
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    constexpr bool MAPB = (ABL & 131072) != 0;
-    const int pos = MAPB ? tg_pos_b(lane) : tg_pos(lane);
+    const int pos = tg_pos(lane);
     char* tabb = tab_all[wv];
     uint32_t* ring = ring_all[wv];
     // This wave's work: chunk blockIdx.x * kWaves + wv, or, in a split launch (Geom::nwhole), piece wv of
@@ -601,13 +548,7 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(7))
     const int aPx = upper5 ? 8 * (3 - L0) + 4 : 8 * L0, aPy = upper5 ? 8 * L0 + 4 : 8 * (3 - L0);
     const int aU0 = aK[0] + (upper5 ? 4 : 0);  // M_B32 phase-0 pair row: this lane's (E-, E+) half
     const int pa5 = 4 * (lane ^ 32);  // ds_bpermute address of the xor-32 partner (tools variant)
-    const f2v spm = (f2v){1.0f, -1.0f};  // [a, b] = [V + m, V - m] of the two-op DPP stage
-    f2v sxp[2];
-    sfor<2>([&](auto W) {
-        constexpr int w = decltype(W)::value;  // 0: K=0 (Q=5), 1: K=5 (Q=4)
-        constexpr int Q = w == 0 ? 5 : 4;
-        sxp[w] = ((pos >> Q) & 1) ? (f2v){-1.0f, 1.0f} : (f2v){1.0f, -1.0f};
-    });
+    const f2v sxp = upper5 ? (f2v){-1.0f, 1.0f} : (f2v){1.0f, -1.0f};  // the xor-32 swap's [sx, -sx]
     // table-build roles: every lane writes row `lane` (stages 0..63 of the group), lanes 0..31 also
     // row 64 + lane; J divides 32, so the tag position (row % J) is lane % J for both
     const uint64_t li = (uint64_t)(lane & 31);
@@ -619,10 +560,9 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(7))
     // bits: V = 1.5*2^23 + metric*2^S + 2^(S-1) + h.  The 2^(S-1) offset keeps the history field
     // 2^(S-1) + h in (0, 2^S), so read-out and clearing are bit operations on the pattern.
     // INT: V = metric*2^S + 2^(S-1) + h as an int32, no base needed.
-    // FM: base 2^30 keeps every pattern and candidate in [2^23, 2^31 - 2^23) (|V - base| < 2^30 * 0.91).
-    constexpr uint32_t VBASE = (INT ? (FM ? 0x40000000u : 0u) : 0x4B400000u) + (1u << (S - 1));  // pattern of 1.5*2^23 + 2^(S-1)
+    constexpr uint32_t VBASE = (INT ? 0u : 0x4B400000u) + (1u << (S - 1));  // pattern of 1.5*2^23 + 2^(S-1)
     const uint32_t fnm = ~((1u << S) - 1u), fhf = 1u << (S - 1);  // field clear: (p & fnm) | fhf
-    Fair<(ABL & (1 << 20)) != 0> fair;  // fairness controller (vd_kernels.h; ABL & 256 disables)
+    Fair fair;  // fairness controller (vd_kernels.h; ABL & 256 disables)
     if constexpr (!(ABL & 256)) fair.begin(geo.fair, lane);
     const uint64_t availB = IN::bytes(geo.availStages);
     const uint32_t vo1 = IN::voff(lane), vo2 = IN::voff((int)li);
@@ -696,41 +636,29 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(7))
             // ABL (tools only): 2 = no table reads, 128 = every stage a DPP stage, 4 = no field read-out
             constexpr bool ODD = (r / 6) % 2 == 1;
             constexpr int RP = TT::pairrow(K) ? r : (ODD ? r - 6 : r);  // where this stage's pair was read
-            // The position bit on lane xor 16 (Q=4; Q=2 with the ABL 131072 map) fetches the partner's
-            // metric through the LDS crossbar (ds_swizzle); Q=5 (xor 32) through ds_bpermute or with the
-            // v_permlane32_swap candidate swap (BP5 above): a VALU lane swap costs ~2 DPP ops of issue, the
-            // LDS exchange one round trip queued behind the table reads.
-            // ABL (tools only): 16384 = xor 16 by v_permlane16_swap too, 8192 = flip the Q=5 choice (BP5).
-            constexpr int X16 = MAPB ? 2 : 4;
-            constexpr bool IS16 = Q == X16, IS32 = Q == 5;
-            constexpr int DCTRL = MAPB && Q == 4 ? 2 : (Q <= 3 ? Q : 3);  // lane xor 1, 2, 7, 8 -> DPP control
-            constexpr bool LSW = (IS32 && BP5) || (IS16 && !(ABL & 16384));
-            if constexpr (INT && (ABL & (1 << 23))) {  // study: the fp32 stages on the int patterns (wrong results)
-                if constexpr (Q <= 3) tg_stage_dpp<Q>(V, ODD ? vp[RP].y : vp[RP].x);
-                else if constexpr (Q == 5) tg_stage_swap<5, 2>(V, vp[RP], sxp[0]);
-                else {
-                    const float pv = __builtin_bit_cast(float, __builtin_amdgcn_ds_swizzle(__builtin_bit_cast(int, V), 0x401F));
-                    tg_stage_lds<0>(V, vp[RP], pv, upper5);
-                }
-            } else if constexpr (INT) {  // int32 patterns (SOFT16): DPP, xor-32 swap (signed pairs), xor-16 swizzle
+            // The position bit on lane xor 16 (Q=4) fetches the partner's metric through the LDS crossbar
+            // (ds_swizzle); Q=5 (xor 32) through ds_bpermute or with the v_permlane32_swap candidate swap
+            // (BP5 above): a VALU lane swap costs ~2 DPP ops of issue, the LDS exchange one round trip
+            // queued behind the table reads.
+            constexpr bool IS16 = Q == 4, IS32 = Q == 5;
+            constexpr int DCTRL = Q <= 3 ? Q : 3;  // lane xor 1, 2, 7, 8 -> DPP control
+            constexpr bool LSW = (IS32 && BP5) || IS16;
+            if constexpr (INT) {  // int32 patterns (SOFT16): DPP, xor-32 swap (signed pairs), xor-16 swizzle
                 // DPP stages in the two-op form (sub, add, max with the partner's b through DPP): 5 %
                 // faster than add, sub_dpp, max on int32 (tools/vd_ablate; ABL 1<<24: the three-op form)
                 if constexpr (Q <= 3 && !(ABL & (1 << 24))) tg_stage_dpp_i2<Q>(V, ODD ? vp[RP].y : vp[RP].x);
-                else if constexpr (Q <= 3) tg_stage_dpp_i<Q, FM>(V, ODD ? vp[RP].y : vp[RP].x);
-                else if constexpr (Q == 5) tg_stage_swap_i<FM>(V, vp[RP]);
+                else if constexpr (Q <= 3) tg_stage_dpp_i<Q>(V, ODD ? vp[RP].y : vp[RP].x);
+                else if constexpr (Q == 5) tg_stage_swap_i(V, vp[RP]);
                 else {
                     const float pv = __builtin_bit_cast(float, __builtin_amdgcn_ds_swizzle(__builtin_bit_cast(int, V), 0x401F));
-                    tg_stage_lds_i<FM>(V, ODD ? vp[RP].y : vp[RP].x, pv);
+                    tg_stage_lds_i(V, ODD ? vp[RP].y : vp[RP].x, pv);
                 }
-            } else if constexpr (((!IS16 && !IS32) || (ABL & 128)) && (DPP2 || (ABL & 524288)) && !TT::pairrow(K)) {
-                // two-op DPP forms: sub, add, max_dpp (DPP2); ABL 524288 (tools) pk_fma, max_dpp
-                const f2v e = (ABL & 2) ? (f2v){(float)aK[K], 1.0f} : vp[RP];
-                tg_stage_dpp2<DCTRL, ODD ? 1 : 0, (ABL & 524288) != 0>(V, e, spm);
+            } else if constexpr (((!IS16 && !IS32) || (ABL & 128)) && DPP2 && !TT::pairrow(K)) {
+                const float m = (ABL & 2) ? (float)aK[K] : (ODD ? vp[RP].y : vp[RP].x);
+                tg_stage_dpp2<DCTRL>(V, m);
             } else if constexpr ((!IS16 && !IS32) || (ABL & 128)) {
                 const float m = (ABL & 2) ? (float)aK[K] : (ODD ? vp[RP].y : vp[RP].x);
-                // ABL 1<<21 (study): no s_nop inside the stage where hipcc pads the asm boundary itself
-                constexpr bool NOPD = !(ABL & (1 << 21)) || i % 16 == 0;
-                tg_stage_dpp<DCTRL, NOPD>(V, m);
+                tg_stage_dpp<DCTRL>(V, m);
             } else if constexpr (LSW && S32 && IS32) {
                 const float pv = tg_partner(V, pa5);
                 const f2v e = (ABL & 2) ? (f2v){(float)aK[K], 1.0f} : vp[RP];
@@ -742,7 +670,7 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(7))
                 tg_stage_lds<TT::pairrow(K) ? (BP5 ? 0 : 2) : (ODD ? 1 : 0)>(V, e, pv, upper5);
             } else {
                 const f2v e = (ABL & 2) ? (f2v){(float)aK[K], 1.0f} : vp[RP];
-                tg_stage_swap<IS16 ? 4 : 5, TT::pairrow(K) ? 2 : (ODD ? 1 : 0), (ABL >> 10) & 7>(V, e, sxp[K == 0 ? 0 : 1]);
+                tg_stage_swap<TT::pairrow(K) ? 2 : (ODD ? 1 : 0)>(V, e, sxp);
             }
             if constexpr (r + TGD < 96) issue(std::integral_constant<int, r + TGD>{});
             if constexpr (i % J == J - 1 && !(ABL & 4)) {

@@ -122,9 +122,7 @@ __device__ __forceinline__ uint32_t simd_slot()
 // and sets its issue priority from its lag behind the mean of the SIMD's waves, read at the previous
 // head.  Posting is a plain store and reading one 64-byte load (16 lanes): both stay in the XCD's L2
 // (all waves of a SIMD are on one XCD), so the board adds no HBM or fabric traffic -- a returning atomic
-// per group went past the L2 and cost 11 MB of writes per launch (profiles/r02).  LD1: read with
-// agent-scope (sc1) loads instead of workgroup-scope (sc0) ones (tools, A/B).
-template <bool LD1 = false>
+// per group went past the L2 and cost 11 MB of writes per launch (profiles/r02).
 struct Fair {
     uint32_t* mine = nullptr;   // this wave's word
     uint32_t* simd = nullptr;   // the SIMD's kFairWaves words
@@ -162,8 +160,7 @@ struct Fair {
         }
         if (lane == 0) __hip_atomic_store(mine, j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
         const uint32_t* w = simd + (lane & (kFairWaves - 1));
-        if constexpr (LD1) seen = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        else seen = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        seen = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
     __device__ __forceinline__ void end(int lane)
     {

@@ -51,10 +51,9 @@ int main(int argc, char** argv)
     tgb<2>(v, "tg hard/b32 -tabreads"); tgb<4>(v, "tg hard/b32 -readout"); tgb<8>(v, "tg hard/b32 -tabbuild"); tgb<128>(v, "tg hard/b32 all-dpp"); tgb<512>(v, "tg hard/b32 -tabwrites"); tgs<512>(v, "tg soft8/b16 -tabwrites"); tgs<8>(v, "tg soft8/b16 -tabbuild");
     tgb<2 | 4 | 8 | 16 | 1>(v, "tg hard/b32 ACS only"); tgb<2 | 4 | 8 | 16 | 1 | 128>(v, "tg hard/b32 ACS only all-dpp");
     tgs<2 | 4 | 8 | 16 | 1>(v, "tg soft8/b16 ACS only");
-    tgi<0>(v, "tg soft16/b32 full"); tgi<(1 << 22)>(v, "tg soft16/b32 fp32 max");
-    tgi<(1 << 23)>(v, "tg soft16/b32 fp32 stages"); tgi<8>(v, "tg soft16/b32 -tabbuild"); tgi<4>(v, "tg soft16/b32 -readout");
+    tgi<0>(v, "tg soft16/b32 full");
+    tgi<8>(v, "tg soft16/b32 -tabbuild"); tgi<4>(v, "tg soft16/b32 -readout");
     tgi<1>(v, "tg soft16/b32 -traceback"); tgi<2 | 4 | 8 | 16 | 1>(v, "tg soft16/b32 ACS only");
-    tgi<2 | 4 | 8 | 16 | 1 | (1 << 23)>(v, "tg soft16/b32 ACS only fp32");
     tgi<(1 << 24)>(v, "tg soft16/b32 dpp three-op");
     psk<vd::HARD, vd::B32, 0>(v, "ps hard/b32 full"); psk<vd::SOFT8, vd::B16, 0>(v, "ps soft8/b16 full");
     psk<vd::SOFT16, vd::B32, 0>(v, "ps soft16/b32 full"); psk<vd::FP32, vd::F16, 0>(v, "ps fp32/f16 full");
@@ -68,11 +67,7 @@ int main(int argc, char** argv)
     v.push_back({"ps soft8/b16 6144 chunks", (KFn)vd::vd_decode_ps<vd::SOFT8, vd::B16, 32, 0>, 768});
     tgs<0>(v, "tg soft8/b16 full"); tgs<1>(v, "tg soft8/b16 -traceback"); tgs<2>(v, "tg soft8/b16 -tabreads"); tgs<4>(v, "tg soft8/b16 -readout"); tgf<0>(v, "tg fp32/f16 full");
     tgb<262144>(v, "tg hard/b32 add+subdpp+max"); tgs<262144>(v, "tg soft8/b16 sub+add+maxdpp");
-    tgb<524288>(v, "tg hard/b32 pkfma+maxdpp"); tgs<524288>(v, "tg soft8/b16 pkfma+maxdpp");
-    tgb<(1 << 20)>(v, "tg hard/b32 board sc1 loads"); tgs<(1 << 20)>(v, "tg soft8/b16 board sc1 loads");
-    tgb<(1 << 21)>(v, "tg hard/b32 dpp no inner nop"); tgs<(1 << 21)>(v, "tg soft8/b16 dpp no inner nop");
-    tgs<8192>(v, "tg soft8/b16 q5 permlane"); tgs<16384>(v, "tg soft8/b16 q4 permlane16");
-    tgs<8192 | 16384>(v, "tg soft8/b16 q5 perm32 q4 perm16");
+    tgs<8192>(v, "tg soft8/b16 q5 permlane");
     tgb<8192>(v, "tg hard/b32 q5 permlane"); tgf<8192>(v, "tg fp32/f16 q5 permlane");
     tgb<8192 | 1>(v, "tg hard/b32 perm32 -traceback"); tgb<8192 | 2>(v, "tg hard/b32 perm32 -tabreads"); tgb<8192 | 4>(v, "tg hard/b32 perm32 -readout");
     tgb<8192 | 8>(v, "tg hard/b32 perm32 -tabbuild"); tgb<8192 | 16>(v, "tg hard/b32 perm32 -loads"); tgb<8192 | 256>(v, "tg hard/b32 perm32 -fairness"); tgb<2 | 4 | 8 | 16 | 1 | 8192>(v, "tg hard/b32 ACS only q5 permlane"); tgs<2 | 4 | 8 | 16 | 1 | 8192>(v, "tg soft8/b16 ACS only q5 permlane");
@@ -82,11 +77,10 @@ int main(int argc, char** argv)
         for (size_t i = 0; i < v.size(); i++) { if (!strcmp(v[i].name, a)) ia = (int)i; if (!strcmp(v[i].name, b)) ib = (int)i; }
         if (ia >= 0 && ib >= 0) v[ib].ref = ia;
     };
-    twin("tg soft16/b32 full", "tg soft16/b32 fp32 max"); twin("tg soft16/b32 full", "tg soft16/b32 dpp three-op");
+    twin("tg soft16/b32 full", "tg soft16/b32 dpp three-op");
     twin("tg hard/b32 full", "ps hard/b32 full"); twin("tg soft8/b16 full", "ps soft8/b16 full");
     twin("tg soft16/b32 full", "ps soft16/b32 full"); twin("tg fp32/f16 full", "ps fp32/f16 full");
-    for (const char* k : {"sub+add+maxdpp", "add+subdpp+max", "pkfma+maxdpp", "board sc1 loads", "dpp no inner nop", "q5 bpermute", "q5 permlane", "q4 permlane16",
-                          "q5 perm32 q4 perm16"}) {
+    for (const char* k : {"sub+add+maxdpp", "add+subdpp+max", "q5 permlane"}) {
         char a[96], b[96];
         snprintf(a, sizeof a, "tg hard/b32 full"); snprintf(b, sizeof b, "tg hard/b32 %s", k); twin(a, b);
         snprintf(a, sizeof a, "tg soft8/b16 full"); snprintf(b, sizeof b, "tg soft8/b16 %s", k); twin(a, b);

@@ -205,7 +205,7 @@ __global__ __launch_bounds__(64 * kPsWaves) void vd_decode_ps(const void* __rest
     const float tg0 = CORE == F16 ? tagv : -tagv;
     constexpr uint32_t VBASE = (INT ? 0u : 0x4B400000u) + (1u << (S - 1));
     const uint32_t fnm = ~((1u << S) - 1u), fhf = 1u << (S - 1);
-    Fair<> fair;
+    Fair fair;
     if constexpr (!(ABL & 256)) fair.begin(geo.fair, lane);
     const uint64_t availB = IN::bytes(geo.availStages);
 
