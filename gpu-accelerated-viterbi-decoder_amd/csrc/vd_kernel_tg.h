@@ -496,14 +496,14 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(7))
     static_assert(!INT || CORE == B32, "int32 patterns: SOFT16 on the int32 core only");
     // xor-32 (Q=5) exchange: the partner's metric through the LDS crossbar (ds_bpermute, then three
     // plain VALU ops) instead of v_permlane32_swap (pk_fma, swap, max).  ABL 8192 (tools): the swap.
-    constexpr bool BP5 = !INT && !(ABL & 8192);
+    constexpr bool BP5 = !(ABL & 8192);
     // M_B32 with the LDS exchange (S32): its phase-0 tie rule differs between the position halves (upper
     // half: own wins, tag +2^j).  Instead of rows holding both tag signs, the upper lanes read the entry of
     // the complementary label in the ordinary row (tag -2^j) and negate it: BM[3-L] = -BM[L], so
     // -(BM[3-L]*2^S - 2^j) = BM[L]*2^S + 2^j.  The stage then forms V + s*e and V_partner - s*e with
     // s = -1 in the upper half (v_fma, as cheap as v_add): the same values as before, and the M_B32 table
     // becomes the M_B16 one (no pair rows: fewer LDS reads and writes).
-    constexpr bool S32 = CORE == B32 && BP5;
+    constexpr bool S32 = CORE == B32 && BP5 && !INT;  // INT keeps the pair rows: the lane reads its half
     // DPP stages as v_sub, v_add, v_max_f32_dpp (the partner's V - m through the DPP operand) instead of
     // v_add, v_sub_f32_dpp, v_max: the same decisions; 1 % faster on M_B32 under bench conditions, no
     // difference elsewhere (profiles/r02/benchab_*.log).  ABL 262144 (tools) flips the choice.
@@ -643,11 +643,12 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(7))
             constexpr bool IS16 = Q == 4, IS32 = Q == 5;
             constexpr int DCTRL = Q <= 3 ? Q : 3;  // lane xor 1, 2, 7, 8 -> DPP control
             constexpr bool LSW = (IS32 && BP5) || IS16;
-            if constexpr (INT) {  // int32 patterns (SOFT16): DPP, xor-32 swap (signed pairs), xor-16 swizzle
+            if constexpr (INT) {  // int32 patterns (SOFT16): DPP, xor-32 bpermute (ABL 8192: swap), xor-16 swizzle
                 // DPP stages in the two-op form (sub, add, max with the partner's b through DPP): 5 %
                 // faster than add, sub_dpp, max on int32 (tools/vd_ablate; ABL 1<<24: the three-op form)
                 if constexpr (Q <= 3 && !(ABL & (1 << 24))) tg_stage_dpp_i2<Q>(V, ODD ? vp[RP].y : vp[RP].x);
                 else if constexpr (Q <= 3) tg_stage_dpp_i<Q>(V, ODD ? vp[RP].y : vp[RP].x);
+                else if constexpr (Q == 5 && BP5) tg_stage_lds_i(V, vp[RP].x, tg_partner(V, pa5));
                 else if constexpr (Q == 5) tg_stage_swap_i(V, vp[RP]);
                 else {
                     const float pv = __builtin_bit_cast(float, __builtin_amdgcn_ds_swizzle(__builtin_bit_cast(int, V), 0x401F));

@@ -49,6 +49,11 @@ def stage(kind, nch=1, stages=24):
                 out += ["v_pk_fma_f32 v[12:13], v[40:41], v[40:41], v[10:11] op_sel_hi:[1,1,0]",
                         "v_pk_fma_f32 v[14:15], v[40:41], v[40:41], v[10:11] op_sel:[0,0,1]",
                         "v_max_f32 v10, v12, v13", "v_max_f32 v11, v14, v15"]
+            elif kind == "pk16 dpp (2 chunks)":  # mov_dpp of the packed pair, pk add / sub / max
+                out += [f"v_mov_b32_dpp {t2}, {V} {QP}", f"v_pk_add_i16 {t1}, {V}, v40", f"v_pk_sub_i16 {t2}, {t2}, v40",
+                        f"v_pk_max_i16 {V}, {t1}, {t2}"]
+            elif kind == "pk16 plain (2 chunks)":  # partner value from elsewhere (LDS): pk add / sub / max
+                out += [f"v_pk_add_i16 {t1}, {V}, v40", f"v_pk_sub_i16 {t2}, v41, v40", f"v_pk_max_i16 {V}, {t1}, {t2}"]
             elif kind == "add+max f32 (no exchange)":
                 out += [f"v_add_f32 {t1}, {V}, v40", f"v_sub_f32 {t2}, {V}, v40", f"v_max_f32 {V}, {t1}, {t2}"]
     return out
@@ -59,6 +64,9 @@ V += [(op, [PK[op].format(a=10 + 2 * (i % 8), b=11 + 2 * (i % 8)) for i in range
 for k in ["3op f32", "2op f32", "3op i32", "2op i32", "swap f32", "add+max f32 (no exchange)"]:
     V.append((f"stage {k}", stage(k), 24))
     V.append((f"stage {k} x2 chains", stage(k, 2), 48))
+for k in ["pk16 dpp (2 chunks)", "pk16 plain (2 chunks)"]:
+    V.append((f"stage {k} per 2 states", stage(k), 24))
+    V.append((f"stage {k} x2 chains per 2 states", stage(k, 2), 48))
 for k in ["2op pk f32 (pair)", "3op pk f32 (pair)", "inlane pk (pair)"]:
     V.append((f"stage {k} per state", stage(k, 2), 48))
 CLB = ','.join(f'"v{i}"' for i in list(range(10, 26)) + [40, 41]) + ', "vcc"'

@@ -51,7 +51,7 @@ int main(int argc, char** argv)
     tgb<2>(v, "tg hard/b32 -tabreads"); tgb<4>(v, "tg hard/b32 -readout"); tgb<8>(v, "tg hard/b32 -tabbuild"); tgb<128>(v, "tg hard/b32 all-dpp"); tgb<512>(v, "tg hard/b32 -tabwrites"); tgs<512>(v, "tg soft8/b16 -tabwrites"); tgs<8>(v, "tg soft8/b16 -tabbuild");
     tgb<2 | 4 | 8 | 16 | 1>(v, "tg hard/b32 ACS only"); tgb<2 | 4 | 8 | 16 | 1 | 128>(v, "tg hard/b32 ACS only all-dpp");
     tgs<2 | 4 | 8 | 16 | 1>(v, "tg soft8/b16 ACS only");
-    tgi<0>(v, "tg soft16/b32 full");
+    tgi<0>(v, "tg soft16/b32 full"); tgi<8192>(v, "tg soft16/b32 q5 permlane");
     tgi<8>(v, "tg soft16/b32 -tabbuild"); tgi<4>(v, "tg soft16/b32 -readout");
     tgi<1>(v, "tg soft16/b32 -traceback"); tgi<2 | 4 | 8 | 16 | 1>(v, "tg soft16/b32 ACS only");
     tgi<(1 << 24)>(v, "tg soft16/b32 dpp three-op");
@@ -77,7 +77,7 @@ int main(int argc, char** argv)
         for (size_t i = 0; i < v.size(); i++) { if (!strcmp(v[i].name, a)) ia = (int)i; if (!strcmp(v[i].name, b)) ib = (int)i; }
         if (ia >= 0 && ib >= 0) v[ib].ref = ia;
     };
-    twin("tg soft16/b32 full", "tg soft16/b32 dpp three-op");
+    twin("tg soft16/b32 full", "tg soft16/b32 dpp three-op"); twin("tg soft16/b32 full", "tg soft16/b32 q5 permlane");
     twin("tg hard/b32 full", "ps hard/b32 full"); twin("tg soft8/b16 full", "ps soft8/b16 full");
     twin("tg soft16/b32 full", "ps soft16/b32 full"); twin("tg fp32/f16 full", "ps fp32/f16 full");
     for (const char* k : {"sub+add+maxdpp", "add+subdpp+max", "q5 permlane"}) {
