@@ -250,8 +250,8 @@ static DeviceState* device_state(int device)
 // SIMDs: 6 whole chunks per SIMD + 256 chunks in 4 pieces) and the chunks are long enough.
 static void plan_split(vd::Geom& g, int options, DeviceState* x)
 {
-    if (out_of(options) != 0) return;  // O_B32 only
-    if (g.packNum / g.nchunks < (uint64_t)vd::kSplitMinWords) return;
+    const uint64_t words32 = out_of(options) != 0 ? g.packNum / 2 : g.packNum;  // O_B16: 16-bit words
+    if (words32 / g.nchunks < (uint64_t)vd::kSplitMinWords) return;
     const uint32_t nsimd = (uint32_t)x->nsimd;
     const uint32_t perSimd = g.nchunks / nsimd, rem = g.nchunks % nsimd, nwhole = g.nchunks - rem;
     if (rem == 0 || rem * vd::kWaves != nsimd || perSimd + 1 > 7) return;

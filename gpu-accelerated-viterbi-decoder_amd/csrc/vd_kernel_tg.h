@@ -451,7 +451,7 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t tg_rsrc(const void* in, uint64
 // <-> state map there.  The pieces of a chunk are the waves of one workgroup (one CU), so all vectors are
 // exchanged through workgroup-visible global memory; nothing leaves the XCD's L2.
 constexpr int kSplitWarm = 6;                // warm-up blocks of a speculative piece (multiple of 3)
-constexpr int kSplitMinWords = 64;           // chunks shorter than this are not split (host side)
+constexpr int kSplitMinWords = 64;           // chunks of fewer 32-bit words are not split (host side)
 constexpr int kSplitVecs = 3 * kWaves;       // per split chunk: start[q], end[parity 0][q], end[parity 1][q]
 struct SplitGeo {
     uint32_t s0, words, E;
@@ -520,7 +520,7 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(7))
     uint32_t* ring = ring_all[wv];
     // This wave's work: chunk blockIdx.x * kWaves + wv, or, in a split launch (Geom::nwhole), piece wv of
     // chunk nwhole + (blockIdx.x - nwhole / kWaves) -- see "split chunks" at the end of the file.
-    const bool split = OB == 32 && geo.nwhole != 0 && blockIdx.x >= geo.nwhole / kWaves;
+    const bool split = geo.nwhole != 0 && blockIdx.x >= geo.nwhole / kWaves;
     const uint32_t chunk = split ? geo.nwhole + (blockIdx.x - geo.nwhole / kWaves) : blockIdx.x * kWaves + wv;
     const int piece = split ? wv : -1;
     const ChunkRange cr = chunk_range(geo, chunk);
@@ -584,8 +584,9 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(7))
         Xspec = sg.Xspec;
         Xcmp = sg.Xcmp;
     }
-    const uint64_t wOut = cr.startWord + s0;  // output word of local word 0 (OB == 32 when split)
-    const uint64_t start = wOut * OB;
+    // local word k = chunk word s0 + k (32-bit words; O_B16 writes each as two 16-bit words)
+    const uint64_t wOut = cr.startWord + s0;  // O_B32: output word of local word 0
+    const uint64_t start = (uint64_t)cr.startWord * OB + 32ull * s0;  // first stage of the run
     const uint32_t nblk = Sw + 2;
     float V = __builtin_bit_cast(float, VBASE);
     // a re-decode starts at the piece's boundary block from its left neighbour's latest end vector
@@ -721,8 +722,9 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(7))
                     ((uint32_t*)out)[wOut + k] = w;
                 } else {
                     uint16_t* o = (uint16_t*)out + cr.startWord;
-                    o[2 * k] = (uint16_t)(w >> 16);
-                    if (2 * k + 1 < cr.words) o[2 * k + 1] = (uint16_t)(w & 0xFFFF);
+                    const uint32_t kc = s0 + k;
+                    o[2 * kc] = (uint16_t)(w >> 16);
+                    if (2 * kc + 1 < cr.words) o[2 * kc + 1] = (uint16_t)(w & 0xFFFF);
                 }
             }
             wave_sync();

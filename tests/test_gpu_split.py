@@ -9,7 +9,7 @@ import os
 import numpy as np
 import pytest
 
-from vitdec import FP32, HARD, M_B16, M_B32, M_FP16, SOFT4, SOFT8, SOFT16
+from vitdec import FP32, HARD, M_B16, M_B32, M_FP16, O_B16, SOFT4, SOFT8, SOFT16
 from test_gpu_parity import gpu_decode, name
 
 
@@ -26,10 +26,13 @@ def decode_split_and_whole(gpu, opt, packed, n):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("opt", [HARD | M_B32, SOFT8 | M_B16, SOFT4 | M_B32, FP32 | M_FP16, SOFT16 | M_B32], ids=name)
+@pytest.mark.parametrize("opt", [HARD | M_B32, SOFT8 | M_B16, SOFT4 | M_B32, FP32 | M_FP16, SOFT16 | M_B32,
+                                 HARD | M_B32 | O_B16, SOFT8 | M_B16 | O_B16, FP32 | M_FP16 | O_B16], ids=name)
 @pytest.mark.parametrize("snr", [0.0, 1.0, 3.0])
 def test_split_equals_whole_16m(gpu, vo, opt, snr):
-    n = 16_000_000  # 78 words per chunk: split (>= 64)
+    # 78 32-bit words per chunk: split (>= 64); O_B16: 156-157 16-bit words per chunk (odd counts: the
+    # last piece writes the chunk's final half word only)
+    n = 16_000_000
     bits, packed = gpu_sim(gpu, opt, n, snr)
     out, whole, redecodes = decode_split_and_whole(gpu, opt, packed, n)
     bad = np.flatnonzero(out != whole)
