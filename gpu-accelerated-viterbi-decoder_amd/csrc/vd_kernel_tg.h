@@ -28,6 +28,7 @@
 // forms a = V + X, b = V + Y in every lane and swaps halves, after which each lane holds its own and
 // its exchanged candidate (X, Y = +-M of the lane and of its partner, from the branch-metric table).
 #pragma once
+#include <type_traits>
 #include "vd_kernels.h"
 #include "vd_pack.h"
 
@@ -283,6 +284,7 @@ template <int CH>
 struct TgIn;
 template <>
 struct TgIn<HARD> {  // 16 stages per word; stage g -> bits 31-2(g%16), 30-2(g%16); g%16 = li%16
+    static constexpr bool FAB = false;  // ab() gives ints
     using raw_t = uint32_t;
     static constexpr int RB = 8;
     static __device__ __forceinline__ uint64_t bytes(uint64_t stages) { return stages / 4; }
@@ -302,6 +304,7 @@ struct TgIn<HARD> {  // 16 stages per word; stage g -> bits 31-2(g%16), 30-2(g%1
 };
 template <>
 struct TgIn<SOFT4> {  // 4 stages per word, byte g%4 from the MSB: high nibble s0, low nibble s1
+    static constexpr bool FAB = false;  // ab() gives ints
     using raw_t = uint32_t;
     static constexpr int RB = 32;
     static __device__ __forceinline__ uint64_t bytes(uint64_t stages) { return stages; }
@@ -321,6 +324,7 @@ struct TgIn<SOFT4> {  // 4 stages per word, byte g%4 from the MSB: high nibble s
 };
 template <>
 struct TgIn<SOFT8> {  // 2 stages per word; the 16-bit half g^1 holds s0 (high byte), s1 (low byte)
+    static constexpr bool FAB = false;  // ab() gives ints
     using raw_t = uint32_t;
     static constexpr int RB = 64;
     static __device__ __forceinline__ uint64_t bytes(uint64_t stages) { return stages * 2; }
@@ -339,6 +343,7 @@ struct TgIn<SOFT8> {  // 2 stages per word; the 16-bit half g^1 holds s0 (high b
 };
 template <>
 struct TgIn<SOFT16> {  // 1 stage per word: high 16 bits s0, low 16 bits s1
+    static constexpr bool FAB = false;  // ab() gives ints
     using raw_t = uint32_t;
     static constexpr int RB = 128;
     static __device__ __forceinline__ uint64_t bytes(uint64_t stages) { return stages * 4; }
@@ -357,6 +362,7 @@ struct TgIn<SOFT16> {  // 1 stage per word: high 16 bits s0, low 16 bits s1
 };
 template <>
 struct TgIn<FP32> {  // 2 floats per stage, clamped to [-8,7]; BM = (int)(+-x0 +- x1) (truncation)
+    static constexpr bool FAB = false;  // ab() gives ints
     using raw_t = float2;
     static constexpr int RB = 256;
     static __device__ __forceinline__ uint64_t bytes(uint64_t stages) { return stages * 8; }
@@ -378,6 +384,8 @@ struct TgIn<FP32> {  // 2 floats per stage, clamped to [-8,7]; BM = (int)(+-x0 +
 // float channel values (2 per stage, 8 bytes), quantised as SoftDecisionPacker(BASE, scale) would
 template <int BASE>
 struct TgInLlr {
+    // SOFT4 / SOFT8: the soft values straight in fp32 (abf), no integer round trip
+    static constexpr bool FAB = BASE == SOFT4 || BASE == SOFT8;
     using raw_t = float2;
     static constexpr int RB = 256;
     static __device__ __forceinline__ uint64_t bytes(uint64_t stages) { return stages * 8; }
@@ -386,6 +394,21 @@ struct TgInLlr {
     static __device__ __forceinline__ raw_t load(__amdgpu_buffer_rsrc_t rs, uint32_t vo)
     {
         return TgIn<FP32>::template load<R>(rs, vo);
+    }
+    // (float)code_value(pack_code(v)) for SOFT4 / SOFT8: rint clamped in fp32 when |v| < 2^31 (exact there),
+    // else the x86 narrowing path of pack_code
+    static __device__ __forceinline__ float soft(float v)
+    {
+        constexpr float lo = BASE == SOFT4 ? -8.0f : -128.0f, hi = BASE == SOFT4 ? 7.0f : 127.0f;
+        if (__builtin_expect(__builtin_fabsf(v) < 2147483648.0f, 1))
+            return __builtin_amdgcn_fmed3f(__builtin_rintf(v), lo, hi);
+        return (float)code_value<BASE>(pack_code<BASE>(v));
+    }
+    static __device__ __forceinline__ void abf(raw_t v, int, float& A, float& B, float scale)
+    {
+        const float s0 = soft(v.x * scale), s1 = soft(v.y * scale);
+        A = s0 + s1;
+        B = s0 - s1;
     }
     static __device__ __forceinline__ void ab(raw_t v, int li, int& A, int& B, float scale)
     {
@@ -737,7 +760,7 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(7))
     // one 96-stage group's table row from the stage's (A, B) = (BM[3], BM[2])
     // table row of stage phase K: E[L] = BM[L]*2^S + tag at entries 0, 2, 4, 6 (the odd dwords are the
     // other period's); M_B32 phase-0 rows: the pairs (E-[L], E+[L]) of both tag signs
-    auto put_row = [&](int rb, int A, int B, int K) {
+    auto put_row = [&](int rb, auto A, auto B, int K) {  // A, B: ints, or floats (IN::FAB)
         if constexpr (INT) {  // int32 entries, the fp32 layout (phase-0 rows: the pairs (E-[L], E+[L]))
             uint32_t* e = (uint32_t*)(tabb + rb);
             const int a = A * (1 << S), b = B * (1 << S), tag = 1 << (lane % J);
@@ -780,11 +803,16 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(7))
         // group head: the table from the inputs loaded one group ago, the next group's loads, then the
         // fairness board (its load returns during this group; nothing here waits on it)
         if constexpr (!(ABL & 8)) {  // ABL 8 (tools only): no table build
-            int A, B;
-            IN::ab(rA, lane, A, B, geo.scale);
+            using ab_t = std::conditional_t<IN::FAB, float, int>;
+            auto ab = [&](const typename IN::raw_t& raw, int l, ab_t& A, ab_t& B) {
+                if constexpr (IN::FAB) IN::abf(raw, l, A, B, geo.scale);
+                else IN::ab(raw, l, A, B, geo.scale);
+            };
+            ab_t A, B;
+            ab(rA, lane, A, B);
             put_row(rowb1, A, B, r6a);
             if (lane < 32) {
-                IN::ab(rB, (int)li, A, B, geo.scale);
+                ab(rB, (int)li, A, B);
                 put_row(rowb2, A, B, r6b);
             }
         }
