@@ -821,7 +821,12 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(7))
             rA = IN::template load<0>(rs, vo1);
             rB = IN::template load<2>(rs, vo2);
         }
-        if constexpr (!(ABL & 256)) fair.group(j, lane);
+        if constexpr (!(ABL & 256)) {
+            // every other group head (6 blocks): 0.7 % faster than every head, every third is 1 % slower
+            // (profiles/r02/benchab_fair.log); ABL 1<<25 (tools): every head
+            constexpr uint32_t FE = (ABL & (1 << 25)) ? 1 : 2;
+            if (FE == 1 || (j / 3) % FE == 0) fair.group<3 * (int)FE>(j, lane);
+        }
         if (split && pass == 0 && (int)j == Xspec) svec[split_start_vec(piece) * 64 + lane] = V;
         if (split && (int)j == Xcmp) svec[split_end_vec(piece, (uint32_t)pass & 1u) * 64 + lane] = V;
         wave_sync();

@@ -118,9 +118,9 @@ __device__ __forceinline__ uint32_t simd_slot()
 
 // Fairness controller.  The SIMD arbiter favours the oldest wave, so left alone the waves sharing a
 // SIMD finish up to 2x apart and the tail of the launch runs at low occupancy (tools/vd_ablate clock
-// stamps).  At every 3-block group head each wave posts the blocks it has started to its own board word
-// and sets its issue priority from its lag behind the mean of the SIMD's waves, read at the previous
-// head.  Posting is a plain store and reading one 64-byte load (16 lanes): both stay in the XCD's L2
+// stamps).  At every other 3-block group head each wave posts the blocks it has started to its own board
+// word and sets its issue priority from its lag behind the mean of the SIMD's waves, read at the
+// previous call.  Posting is a plain store and reading one 64-byte load (16 lanes): both stay in the XCD's L2
 // (all waves of a SIMD are on one XCD), so the board adds no HBM or fabric traffic -- a returning atomic
 // per group went past the L2 and cost 11 MB of writes per launch (profiles/r02).
 struct Fair {
@@ -136,7 +136,8 @@ struct Fair {
         mine = simd + wid;
         if (lane == 0) __hip_atomic_store(mine, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
     }
-    // group head; j = blocks started so far (a multiple of 3)
+    // group head; j = blocks started so far (a multiple of 3); PREV = blocks since the previous call
+    template <int PREV = 3>
     __device__ __forceinline__ void group(uint32_t j, int lane)
     {
         if (!mine) return;
@@ -150,9 +151,9 @@ struct Fair {
             x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xF, 0xF, true);
             x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xF, 0xF, true);
             const uint32_t sum = (uint32_t)__builtin_amdgcn_readlane((int)x, 15);
-            // (own - mean) * n in blocks; own word read back as posted at the previous head (j - 3).
+            // (own - mean) * n in blocks; own word read back as posted at the previous call (j - PREV).
             // 32-bit scalar arithmetic (n <= 16, j < 2^26): 64-bit compares would run on the VALU.
-            const int32_t d = (int32_t)(j - 3) * (int32_t)n - (int32_t)sum, n3 = 3 * (int32_t)n;
+            const int32_t d = (int32_t)(j - PREV) * (int32_t)n - (int32_t)sum, n3 = 3 * (int32_t)n;
             if (d <= -n3) __builtin_amdgcn_s_setprio(3);
             else if (d <= 0) __builtin_amdgcn_s_setprio(2);
             else if (d <= n3) __builtin_amdgcn_s_setprio(1);
