@@ -92,6 +92,40 @@ int main(int argc, char** argv)
             CK(hipEventElapsedTime(&b, ev[1], ev[2]));
             if (r) { th[v].push_back(a / steps); ts[v].push_back(b / steps); }
         }
+    // the product kernels with the two workloads on two streams (independent batches overlap their
+    // launch tails) against the same launches on one stream, alternating
+    {
+        hipStream_t sa, sb;
+        CK(hipStreamCreateWithFlags(&sa, hipStreamNonBlocking));
+        CK(hipStreamCreateWithFlags(&sb, hipStreamNonBlocking));
+        hipEvent_t e0, e1, eb;
+        CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1)); CK(hipEventCreate(&eb));
+        vd::Geom g2 = g;  // the second stream's split launches use their own vector slot
+        float* spec2; CK(hipMalloc(&spec2, 256 * vd::kSplitVecs * 64 * 4));
+        g2.spec = spec2;
+        void* out2; CK(hipMalloc(&out2, 16u << 20));
+        std::vector<float> t1, t2;
+        for (int r = 0; r < groups + 1; r++) {
+            for (int mode = 0; mode < 2; mode++) {
+                CK(hipEventRecord(e0, sa));
+                CK(hipStreamWaitEvent(sb, e0, 0));
+                for (int k = 0; k < steps; k++) {
+                    hipLaunchKernelGGL(vs[0].hard, dim3(1792), dim3(256), 0, sa, inH, out, g);
+                    hipLaunchKernelGGL(vs[0].soft8, dim3(1792), dim3(256), 0, mode ? sb : sa, inS, out2, g2);
+                }
+                CK(hipEventRecord(eb, sb));
+                CK(hipStreamWaitEvent(sa, eb, 0));
+                CK(hipEventRecord(e1, sa));
+                CK(hipEventSynchronize(e1));
+                float ms; CK(hipEventElapsedTime(&ms, e0, e1));
+                if (r) (mode ? t2 : t1).push_back(ms / steps);
+            }
+        }
+        std::sort(t1.begin(), t1.end()); std::sort(t2.begin(), t2.end());
+        const double a = t1[t1.size() / 2], b = t2[t2.size() / 2];
+        printf("step on one stream %.4f ms (%.1f Gb/s), two streams %.4f ms (%.1f Gb/s)\n", a,
+               2.0 * (double)(g.packNum * 32) / (a * 1e-3) / 1e9, b, 2.0 * (double)(g.packNum * 32) / (b * 1e-3) / 1e9);
+    }
     uint32_t redec = 0;
     CK(hipMemcpy(&redec, stats, 4, hipMemcpyDeviceToHost));
     printf("%d groups x %d steps, BSC p %.3f, noise x %.2f, split launches, re-decoded split chunks: %u\n", groups, steps,
