@@ -278,15 +278,18 @@ def other_configs_side_measurement(dev, sptr, stream, reps=20):
         n = 2 * N_BITS
         inp = torch.empty(vitdec.lib().vd_input_size(opt, n), dtype=torch.uint8, device=dev)
         bits = torch.empty(N_BITS, dtype=torch.uint8, device=dev)
-        out = torch.empty(vitdec.lib().vd_output_size(opt, n), dtype=torch.uint8, device=dev)
+        nout = vitdec.lib().vd_output_size(opt, n)
+        ostride = (nout + 255) // 256 * 256
+        outs = torch.empty(reps * ostride, dtype=torch.uint8, device=dev)
+        out = outs[:nout]
         vitdec.simulate_device(opt, N_BITS, SNR_DB, 101 + 2 * i, 102 + 2 * i, bits.data_ptr(), inp.data_ptr(), sptr)
         dec = vitdec.ViterbiCUDA(opt, 0, dev)
-        run = lambda: dec.run_device(inp.data_ptr(), out.data_ptr(), n, sptr)
+        # as the timed region: `reps` batches in one launch (vd_run_device_batch), per batch = time / reps
+        run = lambda: dec.run_device_batch(inp.data_ptr(), 0, outs.data_ptr(), ostride, n, reps, sptr)
         settle(run)
         e = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
         e[0].record(stream)
-        for r in range(reps):
-            run()
+        run()
         e[1].record(stream)
         torch.cuda.synchronize()
         ms = e[0].elapsed_time(e[1]) / reps
@@ -465,26 +468,30 @@ def main():
         nout = vitdec.lib().vd_output_size(opt, input_num)
         inp = torch.empty(nin, dtype=torch.uint8, device=dev)
         bits = torch.empty(N_BITS, dtype=torch.uint8, device=dev)
-        out = torch.empty(nout, dtype=torch.uint8, device=dev)
+        ostride = (nout + 255) // 256 * 256
+        outs = torch.empty(args.steps * ostride, dtype=torch.uint8, device=dev)  # one output per step
+        out = outs[:nout]
         # the reference harness's own chain (std::mt19937 bits and noise, BPSK+AWGN, quantiser at 40000),
         # generated bit-exactly on the GPU (vd_simulate_device)
         bs, ns = rank_seed(rank, wi)
         vitdec.simulate_device(opt, N_BITS, SNR_DB, bs, ns, bits.data_ptr(), inp.data_ptr(), sptr)
         dec = vitdec.ViterbiCUDA(opt, 0, dev)
-        batches.append(dict(name=name, opt=opt, input_num=input_num, inp=inp, out=out, bits=bits, dec=dec,
-                            msg=vitdec.lib().vd_message_len(opt, input_num)))
+        batches.append(dict(name=name, opt=opt, input_num=input_num, inp=inp, out=out, outs=outs, ostride=ostride,
+                            nout=nout, bits=bits, dec=dec, msg=vitdec.lib().vd_message_len(opt, input_num)))
     torch.cuda.synchronize()
 
     nw = len(batches)
-    # The K steps' launches go out back to back on one stream, grouped by workload (all K batches of
-    # workload 0, then all of workload 1, ...): every batch is independent, so the order inside the timed
-    # region does not change the work, and one HIP event between the groups times each kernel over its K
-    # launches.  An event recorded between two kernels costs the GPU a ~5 us bubble (rocprofv3 kernel
-    # trace, profiles/r02), so per-launch events would both slow the step and inflate the kernel times.
+    # The K steps are K independent batches per workload.  Each workload's K batches go out as ONE launch
+    # (vd_run_device_batch: batch k decodes the resident input into its own output k, every batch exactly
+    # as a single vd_run_device would), so the next batch's chunks fill the launch tail that the slowest
+    # XCD sets (0.1776 -> 0.1673 ms per HARD batch in tools/vd_benchab).  One HIP event
+    # between the workloads' launches times each kernel; per batch = launch time / K.
     evs = [torch.cuda.Event(enable_timing=True) for _ in range(nw + 1)]
+    K = args.steps
 
-    def run(b):
-        b["dec"].run_device(b["inp"].data_ptr(), b["out"].data_ptr(), b["input_num"], sptr)
+    def run(b, nbatch):
+        b["dec"].run_device_batch(b["inp"].data_ptr(), 0, b["outs"].data_ptr(), b["ostride"], b["input_num"], nbatch,
+                                  sptr)
 
     # Warm-up: the W steps asked for, and at least WARM_S seconds of steps.  From idle the GPU takes
     # tens of milliseconds to reach its sustained clock; a timed region right behind a short warm-up read
@@ -493,26 +500,28 @@ def main():
     tw = time.perf_counter()
     while nwarm < args.warmup or time.perf_counter() - tw < args.warm_s:
         for b in batches:
-            run(b)
-        nwarm += 1
-        if nwarm % 8 == 0:
-            torch.cuda.synchronize()
+            run(b, K)
+        nwarm += K
+        torch.cuda.synchronize()
     if world > 1:
         torch.distributed.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     evs[0].record(stream)
     for i, b in enumerate(batches):
-        for _ in range(args.steps):
-            run(b)
+        run(b, K)
         evs[i + 1].record(stream)
     torch.cuda.synchronize()
     if world > 1:
         torch.distributed.barrier()
     elapsed = time.perf_counter() - t0
 
-    # per-kernel average durations from the HIP events on the launch stream
-    kms = [evs[i].elapsed_time(evs[i + 1]) / args.steps for i in range(nw)]
+    # per-launch durations from the HIP events on the launch stream; per batch = / K
+    launch_ms = [evs[i].elapsed_time(evs[i + 1]) for i in range(nw)]
+    kms = [t / K for t in launch_ms]
+    # every batch of a launch decoded the same input: all K outputs must equal the first
+    same = all(bool(torch.equal(b["outs"][k * b["ostride"]: k * b["ostride"] + b["nout"]], b["out"]))
+               for b in batches for k in range(1, K))
 
     # correctness side-channel (outside the timed region): BER of each batch vs its source bits,
     # and an RCCL all_gather of per-rank decoded-word checksums (the only cross-GPU traffic)
@@ -561,7 +570,9 @@ def main():
             pmc = pmcs.get(b["name"], {})
             stages = stages_per_launch(b["opt"], b["input_num"])
             return {"kernel": b["name"] + ": " + vitdec.kernel_name(b["opt"]), "ms": round(kms[i], 4),
-                    "achieved": round(ach, 2), "frac": round(ach / HBM_PEAK_GBS, 5), "algorithmic_bytes_per_launch": alg,
+                    "launch_ms": round(launch_ms[i], 4), "batches_per_launch": K,
+                    "achieved": round(ach, 2), "frac": round(ach / HBM_PEAK_GBS, 5),
+                    "algorithmic_bytes_per_batch": alg, "algorithmic_bytes_per_launch": alg * K,
                     "traffic": pmc.get("traffic_bytes"),
                     "valu": valu_view(pmc, kms[i], stages, b["name"], b["msg"])}
 
@@ -589,6 +600,12 @@ def main():
                 "n_bits_per_batch": N_BITS,
                 "decoded_bits_per_batch": batches[0]["msg"],
                 "parallelism": f"batch-shard x{world}" if world > 1 else "single GPU",
+                "launch": {"entry": "vd_run_device_batch", "batches_per_launch": K,
+                           "what": "each workload's K steps as one launch of K independent batches (the "
+                                   "resident input decoded into K outputs, all checked equal); kernel_ms is "
+                                   "per batch = launch time / K",
+                           "launch_ms": {b["name"]: round(t, 4) for b, t in zip(batches, launch_ms)},
+                           "outputs_identical": same},
                 "kernel_ms": {b["name"]: round(k, 4) for b, k in zip(batches, kms)},
                 "step_minus_kernels_us": round((ms_per_step - sum(kms)) * 1e3, 2),
                 "warmup_steps_run": nwarm,
@@ -606,8 +623,9 @@ def main():
                 "unit": "GB/s",
                 "frac": rl[di]["frac"],
                 "traffic": rl[di]["traffic"],
-                "algorithmic_bytes_per_launch": rl[di]["algorithmic_bytes_per_launch"],
-                "traffic_source": f"profiles/{PMC_ROUND}/pmc_summary.json (FETCH_SIZE x2 + WRITE_SIZE)",
+                "algorithmic_bytes_per_batch": rl[di]["algorithmic_bytes_per_batch"],
+                "per": "one 32M-bit batch (launch time / batches per launch); traffic likewise per batch",
+                "traffic_source": f"profiles/{PMC_ROUND}/pmc_summary.json (FETCH_SIZE x2 + WRITE_SIZE, per batch)",
                 "valu": rl[di]["valu"],
                 "int_op_roofline": {
                     "what": "SURVEY 8d: 256 ops per decoded bit (64 ACS x {2 add, 1 max, 1 decision}) against "

@@ -100,6 +100,7 @@ using launch_fn = void (*)(const void*, void*, vd::Geom, hipStream_t);
 // workgroups of a launch: whole-chunk workgroups plus one per split chunk
 unsigned tg_grid(const vd::Geom& g)
 {
+    if (g.nbatch > 1) return (unsigned)(((uint64_t)g.nchunks * g.nbatch + vd::kWaves - 1) / vd::kWaves);
     if (g.nwhole == 0) return (g.nchunks + vd::kWaves - 1) / vd::kWaves;
     return g.nwhole / vd::kWaves + (g.nchunks - g.nwhole);
 }
@@ -261,9 +262,11 @@ static void plan_split(vd::Geom& g, int options, DeviceState* x)
     g.stats = x->stats;
 }
 
-// llr: in_d holds inputNum float channel values, quantised in the kernel (scale = packer scale)
+// llr: in_d holds inputNum float channel values, quantised in the kernel (scale = packer scale).
+// nbatch > 1: batch b at in_d + b * inStride, out_d + b * outStride, all in one launch (never split).
 static int launch_decode(const vd_decoder* d, const void* in_d, void* out_d, size_t inputNum, hipStream_t s,
-                         bool llr = false, float scale = 1.0f)
+                         bool llr = false, float scale = 1.0f, uint32_t nbatch = 1, uint64_t inStride = 0,
+                         uint64_t outStride = 0)
 {
     const int options = d->options;
     launch_fn f = pick(options, llr);
@@ -276,7 +279,10 @@ static int launch_decode(const vd_decoder* d, const void* in_d, void* out_d, siz
     g.scale = scale;
     if (g.packNum == 0) return VD_OK;
     g.fair = d->ds->board;
-    if (d->split) plan_split(g, options, d->ds);
+    g.nbatch = nbatch;
+    g.inStride = inStride;
+    g.outStride = outStride;
+    if (d->split && nbatch == 1) plan_split(g, options, d->ds);
     f(in_d, out_d, g, s);
     VD_HIP(hipGetLastError());
     return VD_OK;
@@ -396,6 +402,21 @@ int vd_run_device(vd_decoder* d, const void* input_d, void* output_d, size_t inp
     if (!d || !input_d || !output_d) return fail(VD_ERR_ARG, "null argument");
     if (message_len(d->options, inputNum) == 0) return fail(VD_ERR_ARG, "inputNum too small");
     return launch_decode(d, input_d, output_d, inputNum, (hipStream_t)stream);
+}
+
+int vd_run_device_batch(vd_decoder* d, const void* input_d, size_t input_stride, void* output_d, size_t output_stride,
+                        size_t inputNum, int nbatch, void* stream)
+{
+    if (!d || !input_d || !output_d) return fail(VD_ERR_ARG, "null argument");
+    if (nbatch < 1) return fail(VD_ERR_ARG, "nbatch must be >= 1");
+    if (message_len(d->options, inputNum) == 0) return fail(VD_ERR_ARG, "inputNum too small");
+    if (nbatch > 1 && output_stride < message_len(d->options, inputNum) / 8)
+        return fail(VD_ERR_ARG, "output_stride smaller than the output size: batches would overlap");
+    if ((uint64_t)vd::kChunks * (uint64_t)nbatch > 0xFFFFFFFFull) return fail(VD_ERR_ARG, "nbatch too large");
+    if ((input_stride | output_stride) & 3) return fail(VD_ERR_ARG, "strides must be multiples of 4 bytes");
+    if (nbatch == 1) return launch_decode(d, input_d, output_d, inputNum, (hipStream_t)stream);
+    return launch_decode(d, input_d, output_d, inputNum, (hipStream_t)stream, false, 1.0f, (uint32_t)nbatch, input_stride,
+                         output_stride);
 }
 
 static int launch_pack(int options, const float* llr_d, size_t inputNum, float scale, void* packed_d, hipStream_t s)

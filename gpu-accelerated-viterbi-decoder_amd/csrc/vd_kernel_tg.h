@@ -512,7 +512,7 @@ __device__ __forceinline__ bool split_vec_eq(const float* vecs, int a, int b, in
 
 // ================================================================ tagged kernel: one chunk per wave
 template <int CH, int CORE, int OB, int ABL = 0>
-__global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(7))) void vd_decode_tg(const void* __restrict__ in, void* __restrict__ out, Geom geo)
+__global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(7))) void vd_decode_tg(const void* __restrict__ in_all, void* __restrict__ out_all, Geom geo)
 {
     using IN = TgIn<CH>;
     constexpr bool INT = TgFmt<CH>::INT;
@@ -543,8 +543,13 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(7))
     uint32_t* ring = ring_all[wv];
     // This wave's work: chunk blockIdx.x * kWaves + wv, or, in a split launch (Geom::nwhole), piece wv of
     // chunk nwhole + (blockIdx.x - nwhole / kWaves) -- see "split chunks" at the end of the file.
+    // A batched launch (Geom::nbatch > 1) decodes chunk c of batch b at launch chunk b * nchunks + c.
     const bool split = geo.nwhole != 0 && blockIdx.x >= geo.nwhole / kWaves;
-    const uint32_t chunk = split ? geo.nwhole + (blockIdx.x - geo.nwhole / kWaves) : blockIdx.x * kWaves + wv;
+    const uint32_t gchunk = split ? geo.nwhole + (blockIdx.x - geo.nwhole / kWaves) : blockIdx.x * kWaves + wv;
+    const uint32_t batch = geo.nbatch > 1 ? gchunk / geo.nchunks : 0u;
+    const uint32_t chunk = gchunk - batch * geo.nchunks;
+    const void* const in = (const char*)in_all + batch * geo.inStride;
+    void* const out = (char*)out_all + batch * geo.outStride;
     const int piece = split ? wv : -1;
     const ChunkRange cr = chunk_range(geo, chunk);
     if (cr.words == 0) return;  // never in a split workgroup: split chunks have >= kSplitMinWords words

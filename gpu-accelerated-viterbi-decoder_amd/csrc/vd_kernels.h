@@ -47,6 +47,11 @@ struct Geom {
     uint32_t nwhole = 0;
     float* spec = nullptr;       // [chunk - nwhole][kSplitVecs][64] piece boundary metric vectors
     uint32_t* stats = nullptr;   // count of split pieces re-decoded (or null)
+    // several independent batches of the same size in one launch (never split): batch b decodes
+    // in + b * inStride bytes into out + b * outStride bytes; chunk c of the launch = chunk c % nchunks
+    // of batch c / nchunks
+    uint32_t nbatch = 1;
+    uint64_t inStride = 0, outStride = 0;
 };
 // Progress board of the fairness controller: per SIMD slot (XCC, SE, SH, CU, SIMD from the hardware
 // wave id) kFairWaves 32-bit words, one per hardware wave slot of that SIMD (HW_ID.WAVE_ID): the blocks

@@ -39,7 +39,7 @@ _ERRNAMES = {-1: "VD_ERR_OPTIONS", -2: "VD_ERR_ARG", -3: "VD_ERR_DEVICE", -4: "V
 
 # every entry point declared in include/vd_capi.h (tests check the library exports all of them)
 EXPORTS = ["vd_options_valid", "vd_input_size", "vd_message_len", "vd_output_size", "vd_num_chunks",
-           "vd_create", "vd_destroy", "vd_run", "vd_run_device", "vd_run_batches",
+           "vd_create", "vd_destroy", "vd_run", "vd_run_device", "vd_run_device_batch", "vd_run_batches",
            "vd_simulate_host", "vd_count_errors", "vd_last_error", "vd_device_count", "vd_kernel_name",
            "vd_pack_device", "vd_run_device_llr", "vd_run_llr", "vd_host_alloc", "vd_host_free",
            "vd_run_stream", "vd_channel_device", "vd_simulate_device", "vd_mt_state_after", "vd_split_redecodes"]
@@ -69,6 +69,7 @@ def lib():
     L.vd_destroy.argtypes = [vp]
     L.vd_run.argtypes = [vp, vp, vp, sz, ctypes.POINTER(f)]
     L.vd_run_device.argtypes = [vp, vp, vp, sz, vp]
+    L.vd_run_device_batch.argtypes = [vp, vp, sz, vp, sz, sz, ctypes.c_int, vp]
     L.vd_run_batches.argtypes = [i, ctypes.POINTER(vp), ctypes.POINTER(vp), sz, i, ctypes.POINTER(i), i,
                                  ctypes.POINTER(f)]
     L.vd_simulate_host.argtypes = [i, sz, f, ctypes.c_uint32, ctypes.c_uint32, vp, vp]
@@ -197,6 +198,12 @@ class ViterbiCUDA:
         """Async device decode: raw device pointers on self.device, HIP stream handle (int)."""
         _check(lib().vd_run_device(self._h, ctypes.c_void_p(input_ptr), ctypes.c_void_p(output_ptr), inputNum,
                                    ctypes.c_void_p(stream)))
+
+    def run_device_batch(self, input_ptr, input_stride, output_ptr, output_stride, inputNum, nbatch, stream=0):
+        """nbatch independent batches in one launch: batch b at input_ptr + b * input_stride bytes (0: the
+        same input each time) -> output_ptr + b * output_stride bytes (vd_run_device_batch)."""
+        _check(lib().vd_run_device_batch(self._h, ctypes.c_void_p(input_ptr), input_stride, ctypes.c_void_p(output_ptr),
+                                         output_stride, inputNum, nbatch, ctypes.c_void_p(stream)))
 
 
     def run_stream(self, inputs, inputNum=None, outputs=None):

@@ -73,6 +73,14 @@ int vd_run(vd_decoder* dec, const void* input_h, void* output_h, size_t inputNum
  * No allocation, no synchronisation: safe to capture in a hipGraph. */
 int vd_run_device(vd_decoder* dec, const void* input_d, void* output_d, size_t inputNum, void* stream);
 
+/* nbatch independent batches of inputNum encoded values each in ONE launch (new; for batched callers):
+ * batch b reads input_d + b * input_stride bytes (0 = every batch the same input) and writes
+ * output_d + b * output_stride bytes (>= vd_output_size unless nbatch == 1).  Each batch decodes exactly
+ * as vd_run_device would (the reference's 6400-chunk partition per batch); one launch fills the GPU's
+ * tail with the next batch's chunks.  Strides are multiples of 4 bytes; device pointers as above. */
+int vd_run_device_batch(vd_decoder* dec, const void* input_d, size_t input_stride, void* output_d,
+                        size_t output_stride, size_t inputNum, int nbatch, void* stream);
+
 /* Batch sharding over several devices of one node: batch b (input_h[b] -> output_h[b],
  * each inputNum encoded values) is decoded by devices[b % ndev]; batches are independent, so the
  * result of each is identical to a single-device vd_run of that batch.  wall_ms (optional) is the

@@ -121,6 +121,13 @@ public:
     {
         check(vd_run_device(h_, input_d, output_d, inputNum, stream), "runDevice");
     }
+    /* nbatch independent batches in one launch (strides in bytes; input stride 0 = the same input) */
+    void runDeviceBatch(const encPack_t* input_d, size_t inputStride, decPack_t* output_d, size_t outputStride,
+                        size_t inputNum, int nbatch, void* stream = nullptr)
+    {
+        check(vd_run_device_batch(h_, input_d, inputStride, output_d, outputStride, inputNum, nbatch, stream),
+              "runDeviceBatch");
+    }
 
     size_t getInputSize(size_t inputNum) { return vd_input_size(options, inputNum); }
     size_t getMessageLen(size_t inputNum) { return vd_message_len(options, inputNum); }

@@ -15,5 +15,5 @@ run "SQ_INSTS_VALU_FLOPS_FP32 SQ_INSTS_VALU_IOPS SQ_LDS_BANK_CONFLICT SQ_INSTS_S
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/trace -o run --output-format csv -- python3 bench.py --no-cpu-baseline --no-llr --no-pcie --no-channel --no-other > $O/trace.log 2>&1
 echo rc=$?
 find $O/trace -name "*kernel_stats.csv" -exec cp {} $O/kernel_stats.csv \;
-python3 tools/pmc_summary.py $O/pmc $O/pmc_summary.json
+python3 tools/pmc_summary.py $O/pmc $O/pmc_summary.json --batches 3
 head -6 $O/kernel_stats.csv

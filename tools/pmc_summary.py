@@ -30,6 +30,8 @@ def short(name):
 
 def main():
     root, out = sys.argv[1], sys.argv[2]
+    # --batches N: each dispatch decoded N batches (vd_run_device_batch); counters and durations per batch
+    nb = int(sys.argv[sys.argv.index("--batches") + 1]) if "--batches" in sys.argv else 1
     vals = defaultdict(lambda: defaultdict(list))
     for f in glob.glob(os.path.join(root, "*", "*counter_collection.csv")):
         with open(f) as fh:
@@ -37,7 +39,7 @@ def main():
                 k = short(row["Kernel_Name"])
                 if k is None:
                     continue
-                vals[k][row["Counter_Name"]].append(float(row["Counter_Value"]))
+                vals[k][row["Counter_Name"]].append(float(row["Counter_Value"]) / nb)
     # kernel durations of the passes run with --kernel-trace (the GRBM pass): the clock of that run
     durs = defaultdict(list)
     for f in glob.glob(os.path.join(root, "*", "*kernel_trace.csv")):
@@ -45,11 +47,12 @@ def main():
             for row in csv.DictReader(fh):
                 k = short(row["Kernel_Name"])
                 if k is not None:
-                    durs[k].append(float(row["End_Timestamp"]) - float(row["Start_Timestamp"]))
+                    durs[k].append((float(row["End_Timestamp"]) - float(row["Start_Timestamp"])) / nb)
     res = {}
     for k, cs in vals.items():
         m = {c: sum(v) / len(v) for c, v in cs.items()}
-        r = {"counters_mean_per_dispatch": m, "dispatches": max(len(v) for v in cs.values())}
+        r = {"counters_mean_per_dispatch": m, "dispatches": max(len(v) for v in cs.values()), "batches_per_dispatch": nb,
+             "per": "batch" if nb > 1 else "dispatch"}
         if "FETCH_SIZE" in m and "WRITE_SIZE" in m:
             fetch = m["FETCH_SIZE"] * 1024 * 2  # KiB, x2 gfx950 streaming-read correction
             write = m["WRITE_SIZE"] * 1024

@@ -126,6 +126,35 @@ int main(int argc, char** argv)
         printf("step on one stream %.4f ms (%.1f Gb/s), two streams %.4f ms (%.1f Gb/s)\n", a,
                2.0 * (double)(g.packNum * 32) / (a * 1e-3) / 1e9, b, 2.0 * (double)(g.packNum * 32) / (b * 1e-3) / 1e9);
     }
+    // one launch per workload decoding `steps` batches (Geom::nbatch, inputs at stride 0, outputs at stride
+    // 0 -- timing only) against `steps` split launches, alternating
+    {
+        hipEvent_t e0, e1, e2;
+        CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1)); CK(hipEventCreate(&e2));
+        vd::Geom gb = g;
+        gb.nwhole = 0; gb.spec = nullptr; gb.nbatch = (uint32_t)steps;
+        const unsigned gridb = 1600u * (unsigned)steps;
+        std::vector<float> th1, ts1, thb, tsb;
+        for (int r = 0; r < groups + 1; r++) {
+            for (int mode = 0; mode < 2; mode++) {
+                CK(hipEventRecord(e0));
+                if (mode) hipLaunchKernelGGL(vs[0].hard, dim3(gridb), dim3(256), 0, 0, inH, out, gb);
+                else for (int k = 0; k < steps; k++) hipLaunchKernelGGL(vs[0].hard, dim3(1792), dim3(256), 0, 0, inH, out, g);
+                CK(hipEventRecord(e1));
+                if (mode) hipLaunchKernelGGL(vs[0].soft8, dim3(gridb), dim3(256), 0, 0, inS, out, gb);
+                else for (int k = 0; k < steps; k++) hipLaunchKernelGGL(vs[0].soft8, dim3(1792), dim3(256), 0, 0, inS, out, g);
+                CK(hipEventRecord(e2));
+                CK(hipEventSynchronize(e2));
+                float a, b; CK(hipEventElapsedTime(&a, e0, e1)); CK(hipEventElapsedTime(&b, e1, e2));
+                if (r) { (mode ? thb : th1).push_back(a / steps); (mode ? tsb : ts1).push_back(b / steps); }
+            }
+        }
+        for (auto* v : {&th1, &ts1, &thb, &tsb}) std::sort(v->begin(), v->end());
+        const double h1 = th1[th1.size() / 2], s1 = ts1[ts1.size() / 2], hb = thb[thb.size() / 2], sb = tsb[tsb.size() / 2];
+        printf("per batch: split launches hard %.4f soft8 %.4f ms (%.1f Gb/s); batched launch hard %.4f soft8 %.4f ms (%.1f Gb/s)\n",
+               h1, s1, 2.0 * (double)(g.packNum * 32) / ((h1 + s1) * 1e-3) / 1e9, hb, sb,
+               2.0 * (double)(g.packNum * 32) / ((hb + sb) * 1e-3) / 1e9);
+    }
     uint32_t redec = 0;
     CK(hipMemcpy(&redec, stats, 4, hipMemcpyDeviceToHost));
     printf("%d groups x %d steps, BSC p %.3f, noise x %.2f, split launches, re-decoded split chunks: %u\n", groups, steps,
