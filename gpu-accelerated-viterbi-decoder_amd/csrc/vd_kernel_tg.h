@@ -37,11 +37,16 @@ namespace vd {
 // channel ids: HARD..FP32 = packed input (viterbiBM.cuh formats); 8 + base = float channel values
 // quantised on the fly exactly like SoftDecisionPacker(base, scale) would have packed them (vd_pack.h)
 constexpr int kLlr = 8;
-template <int CH>
+// I16 (ABL bit 26, tools): SOFT4 / SOFT8 / FP32 on int32 patterns with 16-stage fields (S = 17): half the
+// field read-outs and traceback reads of J = 8; 7168 * 2^17 < 2^30 keeps |V +- E| < 2^31.
+constexpr int kAblI16 = 1 << 26;
+constexpr int kAblPf2 = 1 << 27;  // tools: input loads two groups ahead
+template <int CH, int ABL = 0>
 struct TgFmt {
-    static constexpr bool INT = (CH & 7) == SOFT16;      // int32 metric patterns instead of fp32
-    static constexpr int J = (CH & 7) == HARD ? 16 : 8;  // stages per history field
-    static constexpr int S = J + 1;                      // metric scale 2^S
+    static constexpr bool I16 = (ABL & kAblI16) && (CH & 7) != HARD && (CH & 7) != SOFT16;
+    static constexpr bool INT = (CH & 7) == SOFT16 || I16;         // int32 metric patterns instead of fp32
+    static constexpr int J = (CH & 7) == HARD || I16 ? 16 : 8;     // stages per history field
+    static constexpr int S = J + 1;                                // metric scale 2^S
 };
 // |metric| relative to position 0's at the last renormalisation (every 16 stages), bounded by
 // (K-1)*(BMmax-BMmin) + 16*BMmax, must stay below 2^(22-S) (V in [2^23, 2^24) with t1/t2 margins):
@@ -515,8 +520,9 @@ template <int CH, int CORE, int OB, int ABL = 0>
 __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(7))) void vd_decode_tg(const void* __restrict__ in_all, void* __restrict__ out_all, Geom geo)
 {
     using IN = TgIn<CH>;
-    constexpr bool INT = TgFmt<CH>::INT;
-    static_assert(!INT || CORE == B32, "int32 patterns: SOFT16 on the int32 core only");
+    using FMT = TgFmt<CH, ABL>;
+    constexpr bool INT = FMT::INT;
+    static_assert(!INT || CORE == B32 || FMT::I16, "int32 patterns: SOFT16 on the int32 core only");
     // xor-32 (Q=5) exchange: the partner's metric through the LDS crossbar (ds_bpermute, then three
     // plain VALU ops) instead of v_permlane32_swap (pk_fma, swap, max).  ABL 8192 (tools): the swap.
     constexpr bool BP5 = !(ABL & 8192);
@@ -532,7 +538,7 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(7))
     // difference elsewhere (profiles/r02/benchab_*.log).  ABL 262144 (tools) flips the choice.
     constexpr bool DPP2 = (CORE == B32) != ((ABL & 262144) != 0);
     using TT = TgTab<S32 ? B16 : CORE>;
-    constexpr int J = TgFmt<CH>::J, S = TgFmt<CH>::S;
+    constexpr int J = FMT::J, S = FMT::S;
     constexpr int TBS = TgRing<CORE>::TBS;
     __shared__ __attribute__((aligned(16))) char tab_all[kWaves][TT::BYTES];
     __shared__ __attribute__((aligned(256))) uint32_t ring_all[kWaves][(TBS + 1) * 64];  // bit 31-s = stage s
@@ -629,6 +635,14 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(7))
     __amdgpu_buffer_rsrc_t rs = tg_rsrc<CH>(in, start + 32ull * j0, availB);
     typename IN::raw_t rA = IN::template load<0>(rs, vo1);  // stage `lane` of the group
     typename IN::raw_t rB = IN::template load<2>(rs, vo2);  // stage 64 + li
+    // PF2 (ABL bit 27, tools): the input loads two groups ahead instead of one
+    constexpr bool PF2 = (ABL & kAblPf2) != 0;
+    typename IN::raw_t rA2{}, rB2{};
+    if constexpr (PF2) {
+        const __amdgpu_buffer_rsrc_t rs2 = tg_rsrc<CH>(in, start + 32ull * (j0 + 3), availB);
+        rA2 = IN::template load<0>(rs2, vo1);
+        rB2 = IN::template load<2>(rs2, vo2);
+    }
 
     // Branch-metric table reads, software-pipelined: the entries of stage r are loaded TGD stages
     // ahead; one ds_read_b64 at an even period also carries the entry of the stage 6 later.  The
@@ -677,7 +691,8 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(7))
                 // faster than add, sub_dpp, max on int32 (tools/vd_ablate; ABL 1<<24: the three-op form)
                 if constexpr (Q <= 3 && !(ABL & (1 << 24))) tg_stage_dpp_i2<Q>(V, ODD ? vp[RP].y : vp[RP].x);
                 else if constexpr (Q <= 3) tg_stage_dpp_i<Q>(V, ODD ? vp[RP].y : vp[RP].x);
-                else if constexpr (Q == 5 && BP5) tg_stage_lds_i(V, vp[RP].x, tg_partner(V, pa5));
+                else if constexpr (Q == 5 && BP5)
+                    tg_stage_lds_i(V, TT::pairrow(K) || !ODD ? vp[RP].x : vp[RP].y, tg_partner(V, pa5));
                 else if constexpr (Q == 5) tg_stage_swap_i(V, vp[RP]);
                 else {
                     const float pv = __builtin_bit_cast(float, __builtin_amdgcn_ds_swizzle(__builtin_bit_cast(int, V), 0x401F));
@@ -768,12 +783,13 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(7))
     auto put_row = [&](int rb, auto A, auto B, int K) {  // A, B: ints, or floats (IN::FAB)
         if constexpr (INT) {  // int32 entries, the fp32 layout (phase-0 rows: the pairs (E-[L], E+[L]))
             uint32_t* e = (uint32_t*)(tabb + rb);
-            const int a = A * (1 << S), b = B * (1 << S), tag = 1 << (lane % J);
+            // the tag of the row's own class: +2^j on the F16 core (own wins ties), -2^j elsewhere
+            const int a = A * (1 << S), b = B * (1 << S), tag = CORE == F16 ? -(1 << (lane % J)) : 1 << (lane % J);
             e[0] = (uint32_t)(-a - tag);
             e[2] = (uint32_t)(-b - tag);
             e[4] = (uint32_t)(b - tag);
             e[6] = (uint32_t)(a - tag);
-            if (K == 0) {
+            if (TT::pairrow(0) && K == 0) {
                 e[1] = (uint32_t)(-a + tag);
                 e[3] = (uint32_t)(-b + tag);
                 e[5] = (uint32_t)(b + tag);
@@ -822,9 +838,17 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(7))
             }
         }
         if constexpr (!(ABL & 16)) {
-            rs = tg_rsrc<CH>(in, start + 32ull * (j + 3), availB);
-            rA = IN::template load<0>(rs, vo1);
-            rB = IN::template load<2>(rs, vo2);
+            if constexpr (PF2) {
+                rA = rA2;
+                rB = rB2;
+                rs = tg_rsrc<CH>(in, start + 32ull * (j + 6), availB);
+                rA2 = IN::template load<0>(rs, vo1);
+                rB2 = IN::template load<2>(rs, vo2);
+            } else {
+                rs = tg_rsrc<CH>(in, start + 32ull * (j + 3), availB);
+                rA = IN::template load<0>(rs, vo1);
+                rB = IN::template load<2>(rs, vo2);
+            }
         }
         if constexpr (!(ABL & 256)) {
             // every other group head (6 blocks): 0.7 % faster than every head, every third is 1 % slower

@@ -8,24 +8,19 @@
 #include <algorithm>
 #include <cstring>
 #include <string>
-#include "vd_sc_kernel.h"
 #include "../gpu-accelerated-viterbi-decoder_amd/csrc/vd_kernel_tg.h"
 #include "vd_ps_kernel.h"
-#include "vd_pk_kernel.h"
 
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP error %s at %d\n", hipGetErrorString(e), __LINE__); exit(1); } } while (0)
 
 using KFn = void (*)(const void*, void*, vd::Geom);
 struct Var { const char* name; KFn fn; int grid; int block = 256; int ref = -1; };  // ref: exact twin
 
-template <int ABL> void addb(std::vector<Var>& v, const char* n) { v.push_back({n, (KFn)vd::vd_decode_sc<vd::HARD, vd::B32, 32, ABL>, 1600}); }
-template <int ABL> void adds(std::vector<Var>& v, const char* n) { v.push_back({n, (KFn)vd::vd_decode_sc<vd::SOFT8, vd::B16, 32, ABL>, 1600}); }
 template <int ABL> void tgb(std::vector<Var>& v, const char* n) { v.push_back({n, (KFn)vd::vd_decode_tg<vd::HARD, vd::B32, 32, ABL>, 1600}); }
 template <int ABL> void tgs(std::vector<Var>& v, const char* n) { v.push_back({n, (KFn)vd::vd_decode_tg<vd::SOFT8, vd::B16, 32, ABL>, 1600}); }
 template <int ABL> void tgf(std::vector<Var>& v, const char* n) { v.push_back({n, (KFn)vd::vd_decode_tg<vd::FP32, vd::F16, 32, ABL>, 1600}); }
 template <int ABL> void tgi(std::vector<Var>& v, const char* n) { v.push_back({n, (KFn)vd::vd_decode_tg<vd::SOFT16, vd::B32, 32, ABL>, 1600}); }
 template <int CH, int CORE, int ABL> void psk(std::vector<Var>& v, const char* n) { v.push_back({n, (KFn)vd::vd_decode_ps<CH, CORE, 32, ABL>, 800}); }
-template <int ABL> void addp(std::vector<Var>& v, const char* n) { v.push_back({n, (KFn)vd::vd_decode_pk<vd::SOFT8, vd::B16, 32, ABL>, 3200, 64}); }
 
 int main(int argc, char** argv)
 {
@@ -45,8 +40,6 @@ int main(int argc, char** argv)
     CK(hipMalloc(&g.fair, vd::kFairBoardWords * 4));
     CK(hipMemset(g.fair, 0xFF, vd::kFairBoardWords * 4));
     std::vector<Var> v;
-    addb<0>(v, "sc hard/b32 full"); addb<1>(v, "sc hard/b32 -traceback");
-    adds<0>(v, "sc soft8/b16 full");
     tgb<0>(v, "tg hard/b32 full"); tgb<1>(v, "tg hard/b32 -traceback"); tgb<16>(v, "tg hard/b32 -loads"); tgb<256>(v, "tg hard/b32 -fairness");
     tgb<2>(v, "tg hard/b32 -tabreads"); tgb<4>(v, "tg hard/b32 -readout"); tgb<8>(v, "tg hard/b32 -tabbuild"); tgb<128>(v, "tg hard/b32 all-dpp"); tgb<512>(v, "tg hard/b32 -tabwrites"); tgs<512>(v, "tg soft8/b16 -tabwrites"); tgs<8>(v, "tg soft8/b16 -tabbuild");
     tgb<2 | 4 | 8 | 16 | 1>(v, "tg hard/b32 ACS only"); tgb<2 | 4 | 8 | 16 | 1 | 128>(v, "tg hard/b32 ACS only all-dpp");
@@ -68,6 +61,12 @@ int main(int argc, char** argv)
     tgs<0>(v, "tg soft8/b16 full"); tgs<1>(v, "tg soft8/b16 -traceback"); tgs<2>(v, "tg soft8/b16 -tabreads"); tgs<4>(v, "tg soft8/b16 -readout"); tgf<0>(v, "tg fp32/f16 full");
     tgb<262144>(v, "tg hard/b32 add+subdpp+max"); tgs<262144>(v, "tg soft8/b16 sub+add+maxdpp");
     tgs<8192>(v, "tg soft8/b16 q5 permlane");
+    tgs<vd::kAblI16>(v, "tg soft8/b16 i16"); tgf<vd::kAblI16>(v, "tg fp32/f16 i16");
+    tgs<vd::kAblI16 | 2 | 4 | 8 | 16 | 1>(v, "tg soft8/b16 i16 ACS only");
+    v.push_back({"tg soft4/b16 full", (KFn)vd::vd_decode_tg<vd::SOFT4, vd::B16, 32, 0>, 1600});
+    v.push_back({"tg soft4/b16 i16", (KFn)vd::vd_decode_tg<vd::SOFT4, vd::B16, 32, vd::kAblI16>, 1600});
+    v.push_back({"tg soft8/b32 full", (KFn)vd::vd_decode_tg<vd::SOFT8, vd::B32, 32, 0>, 1600});
+    v.push_back({"tg soft8/b32 i16", (KFn)vd::vd_decode_tg<vd::SOFT8, vd::B32, 32, vd::kAblI16>, 1600});
     tgb<8192>(v, "tg hard/b32 q5 permlane"); tgf<8192>(v, "tg fp32/f16 q5 permlane");
     tgb<8192 | 1>(v, "tg hard/b32 perm32 -traceback"); tgb<8192 | 2>(v, "tg hard/b32 perm32 -tabreads"); tgb<8192 | 4>(v, "tg hard/b32 perm32 -readout");
     tgb<8192 | 8>(v, "tg hard/b32 perm32 -tabbuild"); tgb<8192 | 16>(v, "tg hard/b32 perm32 -loads"); tgb<8192 | 256>(v, "tg hard/b32 perm32 -fairness"); tgb<2 | 4 | 8 | 16 | 1 | 8192>(v, "tg hard/b32 ACS only q5 permlane"); tgs<2 | 4 | 8 | 16 | 1 | 8192>(v, "tg soft8/b16 ACS only q5 permlane");
@@ -80,7 +79,9 @@ int main(int argc, char** argv)
     twin("tg soft16/b32 full", "tg soft16/b32 dpp three-op"); twin("tg soft16/b32 full", "tg soft16/b32 q5 permlane");
     twin("tg hard/b32 full", "ps hard/b32 full"); twin("tg soft8/b16 full", "ps soft8/b16 full");
     twin("tg soft16/b32 full", "ps soft16/b32 full"); twin("tg fp32/f16 full", "ps fp32/f16 full");
-    for (const char* k : {"sub+add+maxdpp", "add+subdpp+max", "q5 permlane"}) {
+    twin("tg fp32/f16 full", "tg fp32/f16 i16"); twin("tg soft4/b16 full", "tg soft4/b16 i16");
+    twin("tg soft8/b32 full", "tg soft8/b32 i16");
+    for (const char* k : {"sub+add+maxdpp", "add+subdpp+max", "q5 permlane", "i16"}) {
         char a[96], b[96];
         snprintf(a, sizeof a, "tg hard/b32 full"); snprintf(b, sizeof b, "tg hard/b32 %s", k); twin(a, b);
         snprintf(a, sizeof a, "tg soft8/b16 full"); snprintf(b, sizeof b, "tg soft8/b16 %s", k); twin(a, b);
@@ -142,8 +143,8 @@ int main(int argc, char** argv)
     }
     // per-wave clock stamps of the full kernel (ABL 32), without and with the priority schedule (64)
     if (argc <= 2)  // not with a filter
-    for (KFn f : {(KFn)vd::vd_decode_sc<vd::HARD, vd::B32, 32, 32>, (KFn)vd::vd_decode_tg<vd::HARD, vd::B32, 32, 32>}) {
-        printf("=== %s\n", f == (KFn)vd::vd_decode_sc<vd::HARD, vd::B32, 32, 32> ? "sc full" : "tg full");
+    for (KFn f : {(KFn)vd::vd_decode_tg<vd::HARD, vd::B32, 32, 32>}) {
+        printf("=== tg full\n");
         for (int r = 0; r < 3; r++) hipLaunchKernelGGL(f, dim3(1600), dim3(256), 0, 0, in, out, g);
         CK(hipDeviceSynchronize());
         std::vector<uint64_t> d(6400 * 6);

@@ -1,5 +1,6 @@
 // vd_benchab.hip -- timing-only A/B of kernel variants under bench conditions (not part of the product):
-// per step one 32M-bit HARD batch (int32 core) and one 32M-bit SOFT8 batch (int16 core), split launches,
+// per step one 32M-bit HARD batch (int32 core) and one 32M-bit SOFT8 batch (int16 core), batched launches
+// over distinct resident copies (the variant table; split launches in the side sections),
 // codeword data (HARD: K=7 codeword through a BSC, p = 0.04; SOFT8: BPSK codeword + Gaussian noise at
 // Eb/N0 2 dB, quantised like SoftDecisionPacker(SOFT8)), K steps back to back with the launches grouped
 // per workload as bench.py does.  Variants alternate step group by step group, so clock and thermal drift
@@ -73,18 +74,37 @@ int main(int argc, char** argv)
         {"product (xor-32 by ds_bpermute)", (KFn)vd::vd_decode_tg<vd::HARD, vd::B32, 32, 0>, (KFn)vd::vd_decode_tg<vd::SOFT8, vd::B16, 32, 0>},
         {"xor-32 by v_permlane32_swap", (KFn)vd::vd_decode_tg<vd::HARD, vd::B32, 32, 8192>, (KFn)vd::vd_decode_tg<vd::SOFT8, vd::B16, 32, 8192>},
         {"fairness every group head (round 2 first half)", (KFn)vd::vd_decode_tg<vd::HARD, vd::B32, 32, (1 << 25)>, (KFn)vd::vd_decode_tg<vd::SOFT8, vd::B16, 32, (1 << 25)>},
+        {"input loads two groups ahead (ABL PF2)", (KFn)vd::vd_decode_tg<vd::HARD, vd::B32, 32, vd::kAblPf2>, (KFn)vd::vd_decode_tg<vd::SOFT8, vd::B16, 32, vd::kAblPf2>},
         {"DPP stage form flipped (HARD add+sub_dpp+max, SOFT8 sub+add+max_dpp)", (KFn)vd::vd_decode_tg<vd::HARD, vd::B32, 32, 262144>, (KFn)vd::vd_decode_tg<vd::SOFT8, vd::B16, 32, 262144>},
     };
     const int nv = sizeof(vs) / sizeof(vs[0]);
+    // bench conditions (bench.py): each workload's `steps` batches as one batched launch, every batch its
+    // own resident copy of the input (distinct addresses: nothing is served from a previous batch's
+    // cache lines), outputs at their own stride
+    const size_t strH = (hh.size() * 4 + 255) / 256 * 256, strS = (hs.size() * 4 + 255) / 256 * 256;
+    const size_t ostr = (g.packNum * 4 + 255) / 256 * 256;
+    void *bH, *bS, *bO;
+    CK(hipMalloc(&bH, strH * steps));
+    CK(hipMalloc(&bS, strS * steps));
+    CK(hipMalloc(&bO, ostr * steps));
+    for (int k = 0; k < steps; k++) {
+        CK(hipMemcpy((char*)bH + k * strH, inH, hh.size() * 4, hipMemcpyDeviceToDevice));
+        CK(hipMemcpy((char*)bS + k * strS, inS, hs.size() * 4, hipMemcpyDeviceToDevice));
+    }
+    vd::Geom gh = g, gs = g;
+    gh.nwhole = gs.nwhole = 0; gh.spec = gs.spec = nullptr;
+    gh.nbatch = gs.nbatch = (uint32_t)steps;
+    gh.inStride = strH; gs.inStride = strS; gh.outStride = gs.outStride = ostr;
+    const unsigned gridB = 1600u * (unsigned)steps;
     hipEvent_t ev[3];
     for (int i = 0; i < 3; i++) CK(hipEventCreate(&ev[i]));
     std::vector<std::vector<float>> th(nv), ts(nv);
     for (int r = 0; r < groups + 1; r++)
         for (int v = 0; v < nv; v++) {
             CK(hipEventRecord(ev[0]));
-            for (int k = 0; k < steps; k++) hipLaunchKernelGGL(vs[v].hard, dim3(1792), dim3(256), 0, 0, inH, out, g);
+            hipLaunchKernelGGL(vs[v].hard, dim3(gridB), dim3(256), 0, 0, bH, bO, gh);
             CK(hipEventRecord(ev[1]));
-            for (int k = 0; k < steps; k++) hipLaunchKernelGGL(vs[v].soft8, dim3(1792), dim3(256), 0, 0, inS, out, g);
+            hipLaunchKernelGGL(vs[v].soft8, dim3(gridB), dim3(256), 0, 0, bS, bO, gs);
             CK(hipEventRecord(ev[2]));
             CK(hipEventSynchronize(ev[2]));
             float a, b;
@@ -92,6 +112,22 @@ int main(int argc, char** argv)
             CK(hipEventElapsedTime(&b, ev[1], ev[2]));
             if (r) { th[v].push_back(a / steps); ts[v].push_back(b / steps); }
         }
+    // exact twins: every variant's words equal the product kernel's (last batch of the launch)
+    {
+        std::vector<uint32_t> a(g.packNum), b(g.packNum);
+        for (int w = 0; w < 2; w++)
+            for (int v = 0; v < nv; v++) {
+                CK(hipMemset(bO, 0, ostr * steps));
+                if (w == 0) hipLaunchKernelGGL(vs[v].hard, dim3(gridB), dim3(256), 0, 0, bH, bO, gh);
+                else hipLaunchKernelGGL(vs[v].soft8, dim3(gridB), dim3(256), 0, 0, bS, bO, gs);
+                CK(hipMemcpy(v ? b.data() : a.data(), (char*)bO + (steps - 1) * ostr, g.packNum * 4, hipMemcpyDeviceToHost));
+                if (v) {
+                    size_t bad = 0;
+                    for (size_t k = 0; k < a.size(); k++) bad += a[k] != b[k];
+                    printf("exact twin %s %-40.40s: %zu words differ\n", w ? "soft8" : "hard ", vs[v].name, bad);
+                }
+            }
+    }
     // the product kernels with the two workloads on two streams (independent batches overlap their
     // launch tails) against the same launches on one stream, alternating
     {
@@ -157,7 +193,7 @@ int main(int argc, char** argv)
     }
     uint32_t redec = 0;
     CK(hipMemcpy(&redec, stats, 4, hipMemcpyDeviceToHost));
-    printf("%d groups x %d steps, BSC p %.3f, noise x %.2f, split launches, re-decoded split chunks: %u\n", groups, steps,
+    printf("%d groups x %d steps, BSC p %.3f, noise x %.2f, variants: batched launches, distinct inputs; split re-decodes: %u\n", groups, steps,
            pflip, nscale, redec);
     for (int v = 0; v < nv; v++) {
         std::sort(th[v].begin(), th[v].end());
