@@ -255,7 +255,7 @@ static void plan_split(vd::Geom& g, int options, DeviceState* x)
     if (words32 / g.nchunks < (uint64_t)vd::kSplitMinWords) return;
     const uint32_t nsimd = (uint32_t)x->nsimd;
     const uint32_t perSimd = g.nchunks / nsimd, rem = g.nchunks % nsimd, nwhole = g.nchunks - rem;
-    if (rem == 0 || rem * vd::kWaves != nsimd || perSimd + 1 > 7) return;
+    if (rem == 0 || rem * vd::kWaves != nsimd || perSimd + 1 > 8) return;  // 8 waves per SIMD (vd_kernel_tg.h TgRing)
     const uint32_t slot = x->next.fetch_add(1) % kSplitSlots;
     g.nwhole = nwhole;
     g.spec = x->spec + (size_t)slot * x->maxSplit * kSpecVecs * 64;

@@ -41,6 +41,7 @@ constexpr int kLlr = 8;
 // field read-outs and traceback reads of J = 8; 7168 * 2^17 < 2^30 keeps |V +- E| < 2^31.
 constexpr int kAblI16 = 1 << 26;
 constexpr int kAblPf2 = 1 << 27;  // tools: input loads two groups ahead
+constexpr int kAbl7w = 1 << 28;   // tools: 13 ring slots per wave, 7 waves per SIMD (before r02's last commits)
 template <int CH, int ABL = 0>
 struct TgFmt {
     static constexpr bool I16 = (ABL & kAblI16) && (CH & 7) != HARD && (CH & 7) != SOFT16;
@@ -76,10 +77,12 @@ struct TgTab {
     }
     static constexpr int BYTES = 8 * 60 * 4;
 };
-// survivor ring slots per wave: table + ring of 4 waves fit 7 workgroups per CU (<= 22.8 KiB each)
+// survivor ring slots per wave: table + ring of 4 waves fit 8 workgroups per CU (19,968 B each), so every
+// SIMD holds 8 waves (61 VGPRs): 1.4 % faster per batch than 13 slots at 7 waves under bench conditions
+// (profiles/r02/benchab_8w.log), the shorter traceback batches included
 template <int CORE>
 struct TgRing {
-    static constexpr int TBS = 13;
+    static constexpr int TBS = 11;
 };
 
 __device__ __forceinline__ int tg_pos(int l)
@@ -517,7 +520,7 @@ __device__ __forceinline__ bool split_vec_eq(const float* vecs, int a, int b, in
 
 // ================================================================ tagged kernel: one chunk per wave
 template <int CH, int CORE, int OB, int ABL = 0>
-__global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(7))) void vd_decode_tg(const void* __restrict__ in_all, void* __restrict__ out_all, Geom geo)
+__global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu((ABL & kAbl7w) ? 7 : 8))) void vd_decode_tg(const void* __restrict__ in_all, void* __restrict__ out_all, Geom geo)
 {
     using IN = TgIn<CH>;
     using FMT = TgFmt<CH, ABL>;
@@ -534,12 +537,12 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(7))
     // becomes the M_B16 one (no pair rows: fewer LDS reads and writes).
     constexpr bool S32 = CORE == B32 && BP5 && !INT;  // INT keeps the pair rows: the lane reads its half
     // DPP stages as v_sub, v_add, v_max_f32_dpp (the partner's V - m through the DPP operand) instead of
-    // v_add, v_sub_f32_dpp, v_max: the same decisions; 1 % faster on M_B32 under bench conditions, no
-    // difference elsewhere (profiles/r02/benchab_*.log).  ABL 262144 (tools) flips the choice.
-    constexpr bool DPP2 = (CORE == B32) != ((ABL & 262144) != 0);
+    // v_add, v_sub_f32_dpp, v_max: the same decisions; 1 % faster on M_B32 and 0.5 % on M_B16 under bench
+    // conditions (profiles/r02/benchab_*.log).  ABL 262144 (tools): the three-op form.
+    constexpr bool DPP2 = (ABL & 262144) == 0;
     using TT = TgTab<S32 ? B16 : CORE>;
     constexpr int J = FMT::J, S = FMT::S;
-    constexpr int TBS = TgRing<CORE>::TBS;
+    constexpr int TBS = (ABL & kAbl7w) ? 13 : TgRing<CORE>::TBS;
     __shared__ __attribute__((aligned(16))) char tab_all[kWaves][TT::BYTES];
     __shared__ __attribute__((aligned(256))) uint32_t ring_all[kWaves][(TBS + 1) * 64];  // bit 31-s = stage s
     const int lane = threadIdx.x & 63;

@@ -72,10 +72,8 @@ int main(int argc, char** argv)
     g.nwhole = 6144; g.spec = spec; g.stats = stats;
     const Variant vs[] = {
         {"product (xor-32 by ds_bpermute)", (KFn)vd::vd_decode_tg<vd::HARD, vd::B32, 32, 0>, (KFn)vd::vd_decode_tg<vd::SOFT8, vd::B16, 32, 0>},
-        {"xor-32 by v_permlane32_swap", (KFn)vd::vd_decode_tg<vd::HARD, vd::B32, 32, 8192>, (KFn)vd::vd_decode_tg<vd::SOFT8, vd::B16, 32, 8192>},
-        {"fairness every group head (round 2 first half)", (KFn)vd::vd_decode_tg<vd::HARD, vd::B32, 32, (1 << 25)>, (KFn)vd::vd_decode_tg<vd::SOFT8, vd::B16, 32, (1 << 25)>},
-        {"input loads two groups ahead (ABL PF2)", (KFn)vd::vd_decode_tg<vd::HARD, vd::B32, 32, vd::kAblPf2>, (KFn)vd::vd_decode_tg<vd::SOFT8, vd::B16, 32, vd::kAblPf2>},
-        {"DPP stage form flipped (HARD add+sub_dpp+max, SOFT8 sub+add+max_dpp)", (KFn)vd::vd_decode_tg<vd::HARD, vd::B32, 32, 262144>, (KFn)vd::vd_decode_tg<vd::SOFT8, vd::B16, 32, 262144>},
+        {"7 waves per SIMD, 13 ring slots (ABL 7W)", (KFn)vd::vd_decode_tg<vd::HARD, vd::B32, 32, vd::kAbl7w>, (KFn)vd::vd_decode_tg<vd::SOFT8, vd::B16, 32, vd::kAbl7w>},
+        {"DPP stages in the three-op form (add, sub_dpp, max)", (KFn)vd::vd_decode_tg<vd::HARD, vd::B32, 32, 262144>, (KFn)vd::vd_decode_tg<vd::SOFT8, vd::B16, 32, 262144>},
     };
     const int nv = sizeof(vs) / sizeof(vs[0]);
     // bench conditions (bench.py): each workload's `steps` batches as one batched launch, every batch its
