@@ -26,17 +26,22 @@ int main(int argc, char** argv)
 {
     const size_t N = 32000000, inputNum = 2 * N;
     const size_t inBytes = inputNum * 4;  // FP32 (largest)
+    // argv[3] = nb > 1: batched launches (bench conditions) of nb batches, each its own copy of the random
+    // input (distinct addresses); only the vd_decode_tg variants run then
+    const int nb = argc > 3 ? std::max(1, atoi(argv[3])) : 1;
+    const size_t outStride = (size_t)4 << 20;
     void *in, *out;
-    CK(hipMalloc(&in, inBytes));
-    CK(hipMalloc(&out, (16u << 20) + 6400 * 48));
+    CK(hipMalloc(&in, inBytes * nb));
+    CK(hipMalloc(&out, std::max((size_t)(16u << 20) + 6400 * 48, outStride * nb)));
     std::vector<uint32_t> h(inBytes / 4);
     uint32_t x = 12345;
     for (auto& w : h) { x ^= x << 13; x ^= x >> 17; x ^= x << 5; w = x; }
-    CK(hipMemcpy(in, h.data(), inBytes, hipMemcpyHostToDevice));
+    for (int b = 0; b < nb; b++) CK(hipMemcpy((char*)in + b * inBytes, h.data(), inBytes, hipMemcpyHostToDevice));
     vd::Geom g;
     g.packNum = (N - 64) / 32;
     g.nchunks = 6400;
     g.availStages = N;
+    if (nb > 1) { g.nbatch = (uint32_t)nb; g.inStride = inBytes; g.outStride = outStride; }
     CK(hipMalloc(&g.fair, vd::kFairBoardWords * 4));
     CK(hipMemset(g.fair, 0xFF, vd::kFairBoardWords * 4));
     std::vector<Var> v;
@@ -105,6 +110,14 @@ int main(int argc, char** argv)
         for (auto& x : w) if (x.ref >= 0) x.ref = idx[x.ref];
         v.swap(w);
     }
+    if (nb > 1) {  // batched: vd_decode_tg variants only, grid x nb, times per batch
+        std::vector<Var> w; std::vector<int> idx(v.size(), -1);
+        for (size_t i = 0; i < v.size(); i++)
+            if (!strncmp(v[i].name, "tg ", 3) && strstr(v[i].name, "6144") == nullptr) { idx[i] = (int)w.size(); w.push_back(v[i]); }
+        for (auto& y : w) { y.ref = y.ref >= 0 ? idx[y.ref] : -1; y.grid *= nb; }
+        v.swap(w);
+        printf("batched launches: %d batches per launch, distinct input copies; times per batch\n", nb);
+    }
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
     const int rounds = argc > 1 ? atoi(argv[1]) : 10;
@@ -116,7 +129,7 @@ int main(int argc, char** argv)
             CK(hipEventRecord(e1));
             CK(hipEventSynchronize(e1));
             float ms; CK(hipEventElapsedTime(&ms, e0, e1));
-            if (r >= 2) t[i].push_back(ms);
+            if (r >= 2) t[i].push_back(ms / nb);
         }
     for (size_t i = 0; i < v.size(); i++) {
         std::sort(t[i].begin(), t[i].end());
@@ -142,7 +155,7 @@ int main(int argc, char** argv)
         }
     }
     // per-wave clock stamps of the full kernel (ABL 32), without and with the priority schedule (64)
-    if (argc <= 2)  // not with a filter
+    if (argc <= 2 && nb == 1)  // not with a filter
     for (KFn f : {(KFn)vd::vd_decode_tg<vd::HARD, vd::B32, 32, 32>}) {
         printf("=== tg full\n");
         for (int r = 0; r < 3; r++) hipLaunchKernelGGL(f, dim3(1600), dim3(256), 0, 0, in, out, g);
