@@ -31,7 +31,7 @@ N_BITS = 32_000_000
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md)
 SNR_DB = 2.0
 WARM_S = 0.5      # minimum warm-up (seconds of steps) before the timed region
-PMC_ROUND = "r02"  # profiles/<round>/pmc_summary.json, profiles/<round>/ablate.log
+PMC_ROUND = "r02"  # profiles/<round>/pmc_summary.json, profiles/<round>/ablate_batched.log
 
 WORKLOADS = [
     ("hard_b32", vitdec.HARD | vitdec.M_B32 | vitdec.O_B32),
@@ -114,11 +114,12 @@ N_XCD = 8         # rocprofv3 sums GRBM_GUI_ACTIVE over the 8 XCDs (MI355X_MICRO
 
 
 def acs_only_ms(name):
-    """Instruction-mix ceiling of a workload's kernel: the time of the same launch with only the ACS
-    recursion left (tools/vd_ablate 'ACS only' variant: no table build/reads, read-out, loads or
-    traceback), from the committed ablation log of this round; None if absent."""
+    """Instruction-mix ceiling of a workload's kernel: the time per batch of the same batched launch with
+    only the ACS recursion left (tools/vd_ablate 'ACS only' variant: no table build/reads, read-out,
+    loads or traceback; 8 batches per launch as the bench launches them), from the committed ablation log
+    of this round; None if absent."""
     key = {"hard_b32": "tg hard/b32 ACS only ", "soft8_b16": "tg soft8/b16 ACS only "}.get(name)
-    p = os.path.join(ROOT, "profiles", PMC_ROUND, "ablate.log")
+    p = os.path.join(ROOT, "profiles", PMC_ROUND, "ablate_batched.log")
     if key is None or not os.path.exists(p):
         return None
     with open(p) as f:
@@ -166,7 +167,7 @@ def valu_view(pmc, kernel_ms, stages, name, msg_bits):
     if acs:
         v["mix_ceiling"] = {"acs_only_ms": acs, "gbps": round(msg_bits / (acs * 1e-3) / 1e9, 2),
                             "frac": round(acs / kernel_ms, 3),
-                            "source": f"profiles/{PMC_ROUND}/ablate.log (random input, unsplit launch)"}
+                            "source": f"profiles/{PMC_ROUND}/ablate_batched.log (random input, 8 batches per launch)"}
     v["source"] = f"profiles/{PMC_ROUND}/pmc_summary.json"
     return v
 

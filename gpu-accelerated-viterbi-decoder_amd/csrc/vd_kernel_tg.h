@@ -40,7 +40,7 @@ constexpr int kLlr = 8;
 // I16 (ABL bit 26, tools): SOFT4 / SOFT8 / FP32 on int32 patterns with 16-stage fields (S = 17): half the
 // field read-outs and traceback reads of J = 8; 7168 * 2^17 < 2^30 keeps |V +- E| < 2^31.
 constexpr int kAblI16 = 1 << 26;
-constexpr int kAblPf2 = 1 << 27;  // tools: input loads two groups ahead
+constexpr int kAblFairAll = 1 << 29;  // tools: fairness controller on every batch of a batched launch
 constexpr int kAbl7w = 1 << 28;   // tools: 13 ring slots per wave, 7 waves per SIMD (before r02's last commits)
 template <int CH, int ABL = 0>
 struct TgFmt {
@@ -587,7 +587,9 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu((AB
     const int pa5 = 4 * (lane ^ 32);  // ds_bpermute address of the xor-32 partner (tools variant)
     const f2v sxp = upper5 ? (f2v){-1.0f, 1.0f} : (f2v){1.0f, -1.0f};  // the xor-32 swap's [sx, -sx]
     // table-build roles: every lane writes row `lane` (stages 0..63 of the group), lanes 0..31 also
-    // row 64 + lane; J divides 32, so the tag position (row % J) is lane % J for both
+    // row 64 + lane; J divides 32, so the tag position (row % J) is lane % J for both.  (Writing rows
+    // 0..59 of the next group a block ahead, when they are dead, measured no faster:
+    // profiles/r02/ablate_twe.log.)
     const uint64_t li = (uint64_t)(lane & 31);
     const float tagv = (float)(1 << (lane % J));
     const float tg0 = CORE == F16 ? tagv : -tagv;  // tag of the row's own class
@@ -600,7 +602,11 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu((AB
     constexpr uint32_t VBASE = (INT ? 0u : 0x4B400000u) + (1u << (S - 1));  // pattern of 1.5*2^23 + 2^(S-1)
     const uint32_t fnm = ~((1u << S) - 1u), fhf = 1u << (S - 1);  // field clear: (p & fnm) | fhf
     Fair fair;  // fairness controller (vd_kernels.h; ABL & 256 disables)
-    if constexpr (!(ABL & 256)) fair.begin(geo.fair, lane);
+    // In a batched launch only the last batch's waves run the controller: earlier batches' waves are
+    // followed by more work on their SIMD, so evening out progress buys nothing there and costs issue
+    // (1.6 % per batch, profiles/r02/benchab_fair2.log).  ABL bit 29 (tools): every batch.
+    if constexpr (!(ABL & 256))
+        fair.begin(!(ABL & kAblFairAll) && batch + 1 < geo.nbatch ? nullptr : geo.fair, lane);
     const uint64_t availB = IN::bytes(geo.availStages);
     const uint32_t vo1 = IN::voff(lane), vo2 = IN::voff((int)li);
     // split workgroups (uniform bookkeeping): bit q of `verified` = piece q checked exact, bit q of
@@ -638,14 +644,6 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu((AB
     __amdgpu_buffer_rsrc_t rs = tg_rsrc<CH>(in, start + 32ull * j0, availB);
     typename IN::raw_t rA = IN::template load<0>(rs, vo1);  // stage `lane` of the group
     typename IN::raw_t rB = IN::template load<2>(rs, vo2);  // stage 64 + li
-    // PF2 (ABL bit 27, tools): the input loads two groups ahead instead of one
-    constexpr bool PF2 = (ABL & kAblPf2) != 0;
-    typename IN::raw_t rA2{}, rB2{};
-    if constexpr (PF2) {
-        const __amdgpu_buffer_rsrc_t rs2 = tg_rsrc<CH>(in, start + 32ull * (j0 + 3), availB);
-        rA2 = IN::template load<0>(rs2, vo1);
-        rB2 = IN::template load<2>(rs2, vo2);
-    }
 
     // Branch-metric table reads, software-pipelined: the entries of stage r are loaded TGD stages
     // ahead; one ds_read_b64 at an even period also carries the entry of the stage 6 later.  The
@@ -787,7 +785,7 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu((AB
         if constexpr (INT) {  // int32 entries, the fp32 layout (phase-0 rows: the pairs (E-[L], E+[L]))
             uint32_t* e = (uint32_t*)(tabb + rb);
             // the tag of the row's own class: +2^j on the F16 core (own wins ties), -2^j elsewhere
-            const int a = A * (1 << S), b = B * (1 << S), tag = CORE == F16 ? -(1 << (lane % J)) : 1 << (lane % J);
+            const int a = A * (1 << S), b = B * (1 << S), tag = -(int)tg0;
             e[0] = (uint32_t)(-a - tag);
             e[2] = (uint32_t)(-b - tag);
             e[4] = (uint32_t)(b - tag);
@@ -841,17 +839,9 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu((AB
             }
         }
         if constexpr (!(ABL & 16)) {
-            if constexpr (PF2) {
-                rA = rA2;
-                rB = rB2;
-                rs = tg_rsrc<CH>(in, start + 32ull * (j + 6), availB);
-                rA2 = IN::template load<0>(rs, vo1);
-                rB2 = IN::template load<2>(rs, vo2);
-            } else {
-                rs = tg_rsrc<CH>(in, start + 32ull * (j + 3), availB);
-                rA = IN::template load<0>(rs, vo1);
-                rB = IN::template load<2>(rs, vo2);
-            }
+            rs = tg_rsrc<CH>(in, start + 32ull * (j + 3), availB);
+            rA = IN::template load<0>(rs, vo1);
+            rB = IN::template load<2>(rs, vo2);
         }
         if constexpr (!(ABL & 256)) {
             // every other group head (6 blocks): 0.7 % faster than every head, every third is 1 % slower
