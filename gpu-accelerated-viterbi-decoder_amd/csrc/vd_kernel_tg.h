@@ -40,6 +40,7 @@ constexpr int kLlr = 8;
 // I16 (ABL bit 26, tools): SOFT4 / SOFT8 / FP32 on int32 patterns with 16-stage fields (S = 17): half the
 // field read-outs and traceback reads of J = 8; 7168 * 2^17 < 2^30 keeps |V +- E| < 2^31.
 constexpr int kAblI16 = 1 << 26;
+constexpr int kAblNoS01 = 1 << 30;    // tools: SOFT8 table rows from (A, B) instead of the two soft values
 constexpr int kAblFairAll = 1 << 29;  // tools: fairness controller on every batch of a batched launch
 constexpr int kAbl7w = 1 << 28;   // tools: 13 ring slots per wave, 7 waves per SIMD (before r02's last commits)
 template <int CH, int ABL = 0>
@@ -348,6 +349,13 @@ struct TgIn<SOFT8> {  // 2 stages per word; the 16-bit half g^1 holds s0 (high b
         A = s0 + s1;
         B = s0 - s1;
     }
+    // the two soft values as floats (sign-extending byte converts): the table row is then six exact FMAs, E[3], E[2] = s1 * +-2^S + (s0 * 2^S + tag), E[0], E[1] = s1 * -+2^S + (-s0 * 2^S + tag)
+    static constexpr bool S01 = true;
+    static __device__ __forceinline__ void s01(raw_t w, float& s0, float& s1)
+    {
+        s0 = (float)(int)(int8_t)(uint8_t)(w >> 8);  // v_lshlrev + v_cvt_f32_i32_sdwa sext BYTE_3
+        s1 = (float)(int)(int8_t)(uint8_t)w;         // v_cvt_f32_i32_sdwa sext BYTE_0
+    }
 };
 template <>
 struct TgIn<SOFT16> {  // 1 stage per word: high 16 bits s0, low 16 bits s1
@@ -389,6 +397,10 @@ struct TgIn<FP32> {  // 2 floats per stage, clamped to [-8,7]; BM = (int)(+-x0 +
         B = (int)__fsub_rn(x0, x1);
     }
 };
+template <class T, class = void>
+struct HasS01 : std::false_type {};
+template <class T>
+struct HasS01<T, std::void_t<decltype(T::S01)>> : std::bool_constant<T::S01> {};
 // float channel values (2 per stage, 8 bytes), quantised as SoftDecisionPacker(BASE, scale) would
 template <int BASE>
 struct TgInLlr {
@@ -820,11 +832,31 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu((AB
             }
         }
     };
+    // S01: rows from the two soft values (six FMAs) instead of (A, B) = (s0 + s1, s0 - s1) (two integer
+    // ops, two converts, four FMAs); fp32 cores without pair rows.  ABL bit 30 (tools): the (A, B) form.
+    constexpr bool S01 = HasS01<IN>::value && !INT && !TT::pairrow(0) && !(ABL & kAblNoS01);
+    auto put_row_s01 = [&](int rb, float s0, float s1) {
+        constexpr float SC = (float)(1 << S);
+        const float X = __builtin_fmaf(s0, SC, tg0), Y = __builtin_fmaf(s0, -SC, tg0);
+        float* e = (float*)(tabb + rb);
+        e[0] = __builtin_fmaf(s1, -SC, Y);
+        e[2] = __builtin_fmaf(s1, SC, Y);
+        e[4] = __builtin_fmaf(s1, -SC, X);
+        e[6] = __builtin_fmaf(s1, SC, X);
+    };
     const int r6a = lane % 6, r6b = (int)(li + 64) % 6;
     for (uint32_t j = j0;; j += 3) {
         // group head: the table from the inputs loaded one group ago, the next group's loads, then the
         // fairness board (its load returns during this group; nothing here waits on it)
-        if constexpr (!(ABL & 8)) {  // ABL 8 (tools only): no table build
+        if constexpr (S01 && !(ABL & 8)) {
+            float s0, s1;
+            IN::s01(rA, s0, s1);
+            put_row_s01(rowb1, s0, s1);
+            if (lane < 32) {
+                IN::s01(rB, s0, s1);
+                put_row_s01(rowb2, s0, s1);
+            }
+        } else if constexpr (!(ABL & 8)) {  // ABL 8 (tools only): no table build
             using ab_t = std::conditional_t<IN::FAB, float, int>;
             auto ab = [&](const typename IN::raw_t& raw, int l, ab_t& A, ab_t& B) {
                 if constexpr (IN::FAB) IN::abf(raw, l, A, B, geo.scale);
