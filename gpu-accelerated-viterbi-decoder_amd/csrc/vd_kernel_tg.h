@@ -12,10 +12,10 @@
 // The history h = sum of the chosen signed digits (+-2^i, i < j) satisfies |h| < 2^j, so on equal
 // metrics the tag decides (the tie rule), and on unequal metrics (a difference of >= 2^S) neither tags
 // nor history can flip the order: every decision equals the reference's int32/int16/fp16 decision.
-// V is kept in [2^23, 2^24) (offset 1.5*2^23), where the fp32 ulp is 1 and the low mantissa bits are
+// V is kept in [2^23, 2^24) (offset 1.25*2^23), where the fp32 ulp is 1 and the low mantissa bits are
 // the low integer bits, and each field starts at 2^(S-1): after J stages the field 2^(S-1) + h is in
 // (0, 2^S), its decision bits (h + 2^J - 1) / 2 are mantissa bits 1..J, and clearing it is one
-// v_and_or_b32.  Renormalising every 16 stages keeps |metric| < 2^(22-S).
+// v_and_or_b32.  Renormalising at the end of every 32-stage block keeps V in range (bounds below).
 //
 // SOFT16 (|BM| up to 65536: a metric spread near 2^21) leaves no room for the tags below 2^24, so its
 // kernel runs the same scheme on int32 patterns (TgFmt::INT): V = metric * 2^S + 2^(S-1) + h with |V| <
@@ -40,6 +40,7 @@ constexpr int kLlr = 8;
 // I16 (ABL bit 26, tools): SOFT4 / SOFT8 / FP32 on int32 patterns with 16-stage fields (S = 17): half the
 // field read-outs and traceback reads of J = 8; 7168 * 2^17 < 2^30 keeps |V +- E| < 2^31.
 constexpr int kAblI16 = 1 << 26;
+constexpr int kAblRn16 = 1 << 27;     // tools: renormalisation every 16 stages around 1.5*2^23
 constexpr int kAblNoS01 = 1 << 30;    // tools: SOFT8 table rows from (A, B) instead of the two soft values
 constexpr int kAblFairAll = 1 << 29;  // tools: fairness controller on every batch of a batched launch
 constexpr int kAbl7w = 1 << 28;   // tools: 13 ring slots per wave, 7 waves per SIMD (before r02's last commits)
@@ -50,10 +51,18 @@ struct TgFmt {
     static constexpr int J = (CH & 7) == HARD || I16 ? 16 : 8;     // stages per history field
     static constexpr int S = J + 1;                                // metric scale 2^S
 };
-// |metric| relative to position 0's at the last renormalisation (every 16 stages), bounded by
-// (K-1)*(BMmax-BMmin) + 16*BMmax, must stay below 2^(22-S) (V in [2^23, 2^24) with t1/t2 margins):
-//   HARD 12+16 = 28 < 32;  SOFT4/FP32 192+256 = 448 < 8192;  SOFT8 3072+4096 = 7168 < 8192.
-// SOFT16 (int32): 6*131070 + 16*65536 = 1,834,996 < 2^21, so |V| < 2^30 and |V +- E| < 2^31.
+// Range.  The largest path metric never decreases (the best state's two successors get +-x, one of
+// them >= it) and grows by at most BMmax per stage; every metric lies within D = (K-1)*(BMmax-BMmin) of
+// the largest.  So R stages after a renormalisation (position 0 at the base, every metric within D of
+// it) the metrics relative to the base are in [-D, D + R*BMmax], and the candidates t1/t2 add
+// +-(BMmax + 1) more, in units of 2^S.  With the base at 1.25*2^23 (2,097,152 above 2^23 and 6,291,456
+// below 2^24) and R = 32:
+//   HARD (BMmax 1; 2^17 units: 16 below, 48 above):  [-14, 12+32+2] fits;
+//   SOFT8 (BMmax 256; 2^9 units: 4096 below, 12288 above):  [-3329, 3072+8192+257] = [-3329, 11521] fits;
+//   SOFT4/FP32 (BMmax 16):  [-209, 192+512+17] fits.
+// SOFT16 (int32, base 0, BMmax 65536, 2^9 units, 2^22 each way): [-851,969, 786,432+2,097,152+65,537]
+// fits, so |V +- E| < 2^31.  The CLI default SNR 15 (saturated soft values on the codeword: the best
+// path gains BMmax every stage) is in the parity tests.  (Until r02's last commits: renormalisation every 16 stages around 1.5*2^23.)
 
 // branch-metric table: per 96-stage group, 16 periods of 6 rows (row K = stage phase); a row holds
 // BM[L]*2^S + c*2^j for the four labels L.  M_B32 rows of phase 0 hold a second set with the other
@@ -611,7 +620,9 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu((AB
     // bits: V = 1.5*2^23 + metric*2^S + 2^(S-1) + h.  The 2^(S-1) offset keeps the history field
     // 2^(S-1) + h in (0, 2^S), so read-out and clearing are bit operations on the pattern.
     // INT: V = metric*2^S + 2^(S-1) + h as an int32, no base needed.
-    constexpr uint32_t VBASE = (INT ? 0u : 0x4B400000u) + (1u << (S - 1));  // pattern of 1.5*2^23 + 2^(S-1)
+    // RN16 (ABL bit 27, tools): renormalise every 16 stages around 1.5*2^23 (before r02's last commits)
+    constexpr bool RN16 = (ABL & kAblRn16) != 0;
+    constexpr uint32_t VBASE = (INT ? 0u : RN16 ? 0x4B400000u : 0x4B200000u) + (1u << (S - 1));  // 1.25*2^23 + 2^(S-1)
     const uint32_t fnm = ~((1u << S) - 1u), fhf = 1u << (S - 1);  // field clear: (p & fnm) | fhf
     Fair fair;  // fairness controller (vd_kernels.h; ABL & 256 disables)
     // In a batched launch only the last batch's waves run the controller: earlier batches' waves are
@@ -734,9 +745,9 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu((AB
             if constexpr (i % J == J - 1 && !(ABL & 4)) {
                 // field read-out: bits 1..J of the pattern, (2^(S-1) + h) >> 1 = (h + 2^J - 1) / 2, go straight
                 // into byte / half g of the block's ring word (SDWA dst_sel: one op for shift and merge), then
-                // the field is cleared to 2^(S-1).  Every 16 stages the decision-neutral renormalisation by
-                // the metric of position 0 follows: readfirstlane (1 wait state after the clear), the
-                // offset on the scalar unit, one vector subtract.
+                // the field is cleared to 2^(S-1).  At the end of every block (32 stages) the decision-neutral
+                // renormalisation by the metric of position 0 follows: readfirstlane (1 wait state after the
+                // clear), the offset on the scalar unit, one vector subtract.
                 constexpr int g = (i % 32) / J;
                 uint32_t sr;
 #define VD_TG_RO(SEL, UNUSED) "v_lshrrev_b32_sdwa %[w], 1, %[V] dst_sel:" SEL " dst_unused:" UNUSED             \
@@ -745,14 +756,18 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu((AB
 #define VD_TG_IN [fnm] "v"(fnm), [fhf] "v"(fhf), [vb] "n"(VBASE)
                 if constexpr (J == 8 && g == 0)
                     asm(VD_TG_RO("BYTE_0", "UNUSED_PAD") : [V] "+{v60}"(V), [w] "=&v"(word) : VD_TG_IN);
-                else if constexpr (J == 8 && g == 1)
+                else if constexpr (J == 8 && g == 1 && RN16)
                     asm(VD_TG_RO("BYTE_1", "UNUSED_PRESERVE") VD_TG_RN : [V] "+{v60}"(V), [w] "+v"(word), [sr] "=&s"(sr) : VD_TG_IN);
+                else if constexpr (J == 8 && g == 1)
+                    asm(VD_TG_RO("BYTE_1", "UNUSED_PRESERVE") : [V] "+{v60}"(V), [w] "+v"(word) : VD_TG_IN);
                 else if constexpr (J == 8 && g == 2)
                     asm(VD_TG_RO("BYTE_2", "UNUSED_PRESERVE") : [V] "+{v60}"(V), [w] "+v"(word) : VD_TG_IN);
                 else if constexpr (J == 8)
                     asm(VD_TG_RO("BYTE_3", "UNUSED_PRESERVE") VD_TG_RN : [V] "+{v60}"(V), [w] "+v"(word), [sr] "=&s"(sr) : VD_TG_IN);
-                else if constexpr (g == 0)
+                else if constexpr (g == 0 && RN16)
                     asm(VD_TG_RO("WORD_0", "UNUSED_PAD") VD_TG_RN : [V] "+{v60}"(V), [w] "=&v"(word), [sr] "=&s"(sr) : VD_TG_IN);
+                else if constexpr (g == 0)
+                    asm(VD_TG_RO("WORD_0", "UNUSED_PAD") : [V] "+{v60}"(V), [w] "=&v"(word) : VD_TG_IN);
                 else
                     asm(VD_TG_RO("WORD_1", "UNUSED_PRESERVE") VD_TG_RN : [V] "+{v60}"(V), [w] "+v"(word), [sr] "=&s"(sr) : VD_TG_IN);
 #undef VD_TG_IN

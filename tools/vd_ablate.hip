@@ -66,6 +66,8 @@ int main(int argc, char** argv)
     tgs<0>(v, "tg soft8/b16 full"); tgs<1>(v, "tg soft8/b16 -traceback"); tgs<2>(v, "tg soft8/b16 -tabreads"); tgs<4>(v, "tg soft8/b16 -readout"); tgf<0>(v, "tg fp32/f16 full");
     tgb<262144>(v, "tg hard/b32 add+subdpp+max"); tgs<262144>(v, "tg soft8/b16 add+subdpp+max");
     tgs<8192>(v, "tg soft8/b16 q5 permlane");
+    tgb<vd::kAblRn16>(v, "tg hard/b32 rn16"); tgs<vd::kAblRn16>(v, "tg soft8/b16 rn16"); tgf<vd::kAblRn16>(v, "tg fp32/f16 rn16");
+    tgi<vd::kAblRn16>(v, "tg soft16/b32 rn16");
     tgs<vd::kAblNoS01>(v, "tg soft8/b16 ab rows"); tgs<vd::kAblNoS01 | 8>(v, "tg soft8/b16 -tabbuild ab");
     tgs<vd::kAblI16>(v, "tg soft8/b16 i16"); tgf<vd::kAblI16>(v, "tg fp32/f16 i16");
     tgs<vd::kAblI16 | 2 | 4 | 8 | 16 | 1>(v, "tg soft8/b16 i16 ACS only");
@@ -85,9 +87,10 @@ int main(int argc, char** argv)
     twin("tg soft16/b32 full", "tg soft16/b32 dpp three-op"); twin("tg soft16/b32 full", "tg soft16/b32 q5 permlane");
     twin("tg hard/b32 full", "ps hard/b32 full"); twin("tg soft8/b16 full", "ps soft8/b16 full");
     twin("tg soft16/b32 full", "ps soft16/b32 full"); twin("tg fp32/f16 full", "ps fp32/f16 full");
-    twin("tg fp32/f16 full", "tg fp32/f16 i16"); twin("tg soft4/b16 full", "tg soft4/b16 i16");
+    twin("tg fp32/f16 full", "tg fp32/f16 i16"); twin("tg fp32/f16 full", "tg fp32/f16 rn16");
+    twin("tg soft16/b32 full", "tg soft16/b32 rn16"); twin("tg soft4/b16 full", "tg soft4/b16 i16");
     twin("tg soft8/b32 full", "tg soft8/b32 i16");
-    for (const char* k : {"add+subdpp+max", "q5 permlane", "i16", "ab rows"}) {
+    for (const char* k : {"add+subdpp+max", "q5 permlane", "i16", "ab rows", "rn16"}) {
         char a[96], b[96];
         snprintf(a, sizeof a, "tg hard/b32 full"); snprintf(b, sizeof b, "tg hard/b32 %s", k); twin(a, b);
         snprintf(a, sizeof a, "tg soft8/b16 full"); snprintf(b, sizeof b, "tg soft8/b16 %s", k); twin(a, b);

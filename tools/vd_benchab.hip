@@ -73,6 +73,7 @@ int main(int argc, char** argv)
     const Variant vs[] = {
         {"product (xor-32 by ds_bpermute)", (KFn)vd::vd_decode_tg<vd::HARD, vd::B32, 32, 0>, (KFn)vd::vd_decode_tg<vd::SOFT8, vd::B16, 32, 0>},
         {"no fairness controller (ABL 256)", (KFn)vd::vd_decode_tg<vd::HARD, vd::B32, 32, 256>, (KFn)vd::vd_decode_tg<vd::SOFT8, vd::B16, 32, 256>},
+        {"renormalisation every 16 stages (ABL 27)", (KFn)vd::vd_decode_tg<vd::HARD, vd::B32, 32, vd::kAblRn16>, (KFn)vd::vd_decode_tg<vd::SOFT8, vd::B16, 32, vd::kAblRn16>},
         {"SOFT8 table rows from (A, B) (ABL 30)", (KFn)vd::vd_decode_tg<vd::HARD, vd::B32, 32, 0>, (KFn)vd::vd_decode_tg<vd::SOFT8, vd::B16, 32, vd::kAblNoS01>},
         {"fairness on every batch (ABL 29)", (KFn)vd::vd_decode_tg<vd::HARD, vd::B32, 32, vd::kAblFairAll>, (KFn)vd::vd_decode_tg<vd::SOFT8, vd::B16, 32, vd::kAblFairAll>},
         {"7 waves per SIMD, 13 ring slots (ABL 7W)", (KFn)vd::vd_decode_tg<vd::HARD, vd::B32, 32, vd::kAbl7w>, (KFn)vd::vd_decode_tg<vd::SOFT8, vd::B16, 32, vd::kAbl7w>},
