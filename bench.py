@@ -143,6 +143,9 @@ def valu_view(pmc, kernel_ms, stages, name, msg_bits):
                      (SIMD-32 model: a wave64 VALU instruction occupies its SIMD for 2 cycles at the
                      least; max/DPP/permlane/bit-field forms take 4 -- profiles/r02/ubench12.log)
       issue_pct_live = the same with the live kernel time at the PMC run's clock
+      cycle_model_pct = 100 * (2 * (SQ_INSTS_VALU_ADD_F32 + _FMA_F32 + _MUL_F32) + 4 * (the other VALU
+                     instructions)) / (1024 * cycles): fp32 add/sub/fma issue in 2 cycles, max, DPP, SDWA,
+                     integer and bit ops in 4 (ubench12.log); _live: at the live kernel time
       mix ceiling  = the same launch with only the ACS recursion (tools/vd_ablate)."""
     c = pmc.get("counters_mean_per_dispatch", {})
     if not c or "SQ_INSTS_VALU" not in c:
@@ -163,6 +166,12 @@ def valu_view(pmc, kernel_ms, stages, name, msg_bits):
             v["pmc_run_clock_ghz"] = round(ghz, 3)
             v["pmc_run_kernel_ms"] = round(pmc["pmc_run_kernel_ns_median"] * 1e-6, 4)
             v["issue_pct_live"] = round(100.0 * insts * 2 / (N_SIMD * kernel_ms * 1e-3 * ghz * 1e9), 1)
+        if "SQ_INSTS_VALU_ADD_F32" in c:
+            two = sum(c.get(k, 0.0) for k in ("SQ_INSTS_VALU_ADD_F32", "SQ_INSTS_VALU_FMA_F32", "SQ_INSTS_VALU_MUL_F32"))
+            mcyc = 2 * two + 4 * (insts - two)
+            v["cycle_model_pct"] = round(100.0 * mcyc / (N_SIMD * cyc), 1)
+            if ghz:
+                v["cycle_model_pct_live"] = round(100.0 * mcyc / (N_SIMD * kernel_ms * 1e-3 * ghz * 1e9), 1)
     acs = acs_only_ms(name)
     if acs:
         v["mix_ceiling"] = {"acs_only_ms": acs, "gbps": round(msg_bits / (acs * 1e-3) / 1e9, 2),

@@ -39,10 +39,12 @@ def test_valu_view_from_committed_pmc():
         assert alg <= p["traffic_bytes"] <= 1.2 * alg, (name, p["traffic_bytes"], alg)
         v = bench.valu_view(p, 0.18, 32_409_536, name, 31_999_936)
         for k in ("insts_per_wave_stage", "issue_pct", "busy_pct", "cycles_per_inst_per_simd", "pmc_run_clock_ghz",
-                  "issue_pct_live", "mix_ceiling"):
+                  "issue_pct_live", "cycle_model_pct", "cycle_model_pct_live", "mix_ceiling"):
             assert k in v, (name, k)
         assert 3.0 < v["insts_per_wave_stage"] < 5.0
         assert 1.5 < v["pmc_run_clock_ghz"] < 2.6
+        # the cycle-weighted VALU model: the binding resource, well above the 2-cycle issue view
+        assert v["issue_pct"] < v["cycle_model_pct"] <= 100.0
 
 
 @pytest.mark.gpu
