@@ -334,6 +334,28 @@ def other_configs_side_measurement(dev, sptr, stream, reps=20):
     return res
 
 
+def single_launch_side_measurement(batches, stream, sptr, reps=20):
+    """The reference run()'s unit of work on device buffers: one vd_run_device launch per 32M-bit batch
+    (split launch, 6400-chunk partition), `reps` of the bench's resident batches back to back, per batch
+    = time / reps.  Outside the timed region; never `value` (the timed region batches its launches)."""
+    res = {}
+    for b in batches:
+        K = b["outs"].numel() // b["ostride"]
+        n = min(reps, K)
+        run = lambda: [b["dec"].run_device(b["inps"].data_ptr() + k * b["istride"],
+                                           b["outs"].data_ptr() + k * b["ostride"], b["input_num"], sptr)
+                       for k in range(n)]
+        settle(run)
+        e = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+        e[0].record(stream)
+        run()
+        e[1].record(stream)
+        torch.cuda.synchronize()
+        ms = e[0].elapsed_time(e[1]) / n
+        res[b["name"]] = {"kernel_ms": round(ms, 4), "gbps": round(b["msg"] / (ms * 1e-3) / 1e9, 2), "launches": n}
+    return res
+
+
 def llr_side_measurement(dev, sptr, stream, reps=20):
     """Float channel values in HBM (the reference's AddNoise output, before SoftDecisionPacker): the GPU
     packer alone, packer + decode, and the fused decode (quantisation in the table build), SOFT8/int16.
@@ -570,6 +592,7 @@ def main():
     pcie = None if (args.no_pcie or rank != 0) else pcie_side_measurement(batches, dev)
     chan = None if (args.no_channel or rank != 0) else channel_side_measurement(dev, sptr)
     other = None if (args.no_other or rank != 0) else other_configs_side_measurement(dev, sptr, stream)
+    single = None if (args.no_other or rank != 0) else single_launch_side_measurement(batches, stream, sptr)
     final_gather = None
     if world > 1:
         elapsed = max_over_ranks(elapsed, dev)
@@ -682,6 +705,8 @@ def main():
             result["config"]["channel_source"] = chan
         if other is not None:
             result["config"]["other_configs"] = other
+        if single is not None:
+            result["config"]["single_launch"] = single
         if final_gather is not None:
             result["config"]["final_gather"] = final_gather
         if not args.no_cpu_baseline and world == 1:
