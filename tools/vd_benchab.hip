@@ -77,6 +77,7 @@ int main(int argc, char** argv)
         {"SOFT8 table rows from (A, B) (ABL 30)", (KFn)vd::vd_decode_tg<vd::HARD, vd::B32, 32, 0>, (KFn)vd::vd_decode_tg<vd::SOFT8, vd::B16, 32, vd::kAblNoS01>},
         {"fairness on every batch (ABL 29)", (KFn)vd::vd_decode_tg<vd::HARD, vd::B32, 32, vd::kAblFairAll>, (KFn)vd::vd_decode_tg<vd::SOFT8, vd::B16, 32, vd::kAblFairAll>},
         {"7 waves per SIMD, 13 ring slots (ABL 7W)", (KFn)vd::vd_decode_tg<vd::HARD, vd::B32, 32, vd::kAbl7w>, (KFn)vd::vd_decode_tg<vd::SOFT8, vd::B16, 32, vd::kAbl7w>},
+        {"8 waves, fairness every batch, renormalisation every 16, (A, B) rows (mid-round state)", (KFn)vd::vd_decode_tg<vd::HARD, vd::B32, 32, vd::kAblFairAll | vd::kAblRn16>, (KFn)vd::vd_decode_tg<vd::SOFT8, vd::B16, 32, vd::kAblFairAll | vd::kAblRn16 | vd::kAblNoS01>},
         {"DPP stages in the three-op form (add, sub_dpp, max)", (KFn)vd::vd_decode_tg<vd::HARD, vd::B32, 32, 262144>, (KFn)vd::vd_decode_tg<vd::SOFT8, vd::B16, 32, 262144>},
     };
     const int nv = sizeof(vs) / sizeof(vs[0]);
@@ -101,8 +102,11 @@ int main(int argc, char** argv)
     hipEvent_t ev[3];
     for (int i = 0; i < 3; i++) CK(hipEventCreate(&ev[i]));
     std::vector<std::vector<float>> th(nv), ts(nv);
+    // the variant order rotates from group to group: a fixed order favoured whichever variant ran last
+    // (0.5-1 %, profiles/r02/benchab_dpp_forms_8w.log)
     for (int r = 0; r < groups + 1; r++)
-        for (int v = 0; v < nv; v++) {
+        for (int vi = 0; vi < nv; vi++) {
+            const int v = (vi + r) % nv;
             CK(hipEventRecord(ev[0]));
             hipLaunchKernelGGL(vs[v].hard, dim3(gridB), dim3(256), 0, 0, bH, bO, gh);
             CK(hipEventRecord(ev[1]));
