@@ -31,6 +31,7 @@ N_BITS = 32_000_000
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md)
 SNR_DB = 2.0
 WARM_S = 0.5      # minimum warm-up (seconds of steps) before the timed region
+POOL = 128        # at most this many resident batches per workload (128 SOFT8 batches: 8.2 GB of input)
 PMC_ROUND = "r02"  # profiles/<round>/pmc_summary.json, profiles/<round>/ablate_batched.log
 
 WORKLOADS = [
@@ -518,17 +519,20 @@ def main():
     stream = torch.cuda.current_stream()
     sptr = stream.cuda_stream
 
-    # resident inputs: each rank synthesises its own K independent batches per workload in HBM (one per
-    # step, each from its own seeds), with the reference harness's own chain (std::mt19937 bits and
-    # noise, BPSK+AWGN, quantiser at 40000) generated bit-exactly on the GPU (vd_simulate_device)
+    # resident inputs: each rank synthesises its own independent batches per workload in HBM (one per
+    # step, each from its own seeds; at most POOL of them, step k decoding batch k % POOL), with the
+    # reference harness's own chain (std::mt19937 bits and noise, BPSK+AWGN, quantiser at 40000)
+    # generated bit-exactly on the GPU (vd_simulate_device)
     K = args.steps
+    P = min(K, POOL)
+    sizes = [P] * (K // P) + ([K % P] if K % P else [])  # batches per launch
     batches = []
     for wi, (name, opt) in enumerate(WORKLOADS):
         input_num = 2 * N_BITS
         nout = vitdec.lib().vd_output_size(opt, input_num)
-        inps, istride, bits = resident_batches(opt, K, lambda k: rank_seed(rank, wi, k, world), dev, sptr)
+        inps, istride, bits = resident_batches(opt, P, lambda k: rank_seed(rank, wi, k, world), dev, sptr)
         ostride = (nout + 255) // 256 * 256
-        outs = torch.empty(K * ostride, dtype=torch.uint8, device=dev)  # one output per step
+        outs = torch.empty(P * ostride, dtype=torch.uint8, device=dev)  # one output per resident batch
         dec = vitdec.ViterbiCUDA(opt, 0, dev)
         nin = vitdec.lib().vd_input_size(opt, input_num)
         # inp / out: batch 0 (the step the CPU baseline and the PCIe side measurement repeat)
@@ -538,16 +542,18 @@ def main():
     torch.cuda.synchronize()
 
     nw = len(batches)
-    # The K steps are K independent batches per workload.  Each workload's K batches go out as ONE launch
+    # The K steps are K independent batches per workload.  Each workload's batches go out as ONE launch
     # (vd_run_device_batch: batch k decodes its own resident input into its own output, every batch
-    # exactly as a single vd_run_device would), so the next batch's chunks fill the launch tail that the
-    # slowest XCD sets (0.1776 -> 0.1673 ms per HARD batch in tools/vd_benchab).  One HIP
-    # event between the workloads' launches times each kernel; per batch = launch time / K.
+    # exactly as a single vd_run_device would; K > POOL: launches of POOL batches), so the next batch's
+    # chunks fill the launch tail that the slowest XCD sets (0.1776 -> 0.1673 ms per HARD
+    # batch in tools/vd_benchab).  One HIP event between the workloads' launches times each kernel; per
+    # batch = launch time / K.
     evs = [torch.cuda.Event(enable_timing=True) for _ in range(nw + 1)]
 
-    def run(b, nbatch):
-        b["dec"].run_device_batch(b["inps"].data_ptr(), b["istride"], b["outs"].data_ptr(), b["ostride"],
-                                  b["input_num"], nbatch, sptr)
+    def run(b):
+        for nbatch in sizes:
+            b["dec"].run_device_batch(b["inps"].data_ptr(), b["istride"], b["outs"].data_ptr(), b["ostride"],
+                                      b["input_num"], nbatch, sptr)
 
     # Warm-up: the W steps asked for, and at least WARM_S seconds of steps.  From idle the GPU takes
     # tens of milliseconds to reach its sustained clock; a timed region right behind a short warm-up read
@@ -556,7 +562,7 @@ def main():
     tw = time.perf_counter()
     while nwarm < args.warmup or time.perf_counter() - tw < args.warm_s:
         for b in batches:
-            run(b, K)
+            run(b)
         nwarm += K
         torch.cuda.synchronize()
     if world > 1:
@@ -565,7 +571,7 @@ def main():
     t0 = time.perf_counter()
     evs[0].record(stream)
     for i, b in enumerate(batches):
-        run(b, K)
+        run(b)
         evs[i + 1].record(stream)
     torch.cuda.synchronize()
     if world > 1:
@@ -576,13 +582,14 @@ def main():
     launch_ms = [evs[i].elapsed_time(evs[i + 1]) for i in range(nw)]
     kms = [t / K for t in launch_ms]
     # correctness side-channel (outside the timed region): the decoded-bit error rate of every batch
-    # against its own source bits (max over the K batches), and an RCCL all_gather of per-rank checksums
-    # of the decoded words (xor over each batch's words, xor over the batches: the only cross-GPU traffic)
+    # against its own source bits (max over the resident batches), and an RCCL all_gather of per-rank
+    # checksums of the decoded words (xor over each batch's words, xor over the batches: the only
+    # cross-GPU traffic)
     bers = []
     sums = []
     for b in batches:
         ber_k, ck = [], 0
-        for k in range(K):
+        for k in range(P):
             e, out_h = batch_ber(b["opt"], b["bits"], b["outs"], b["ostride"], b["nout"], k, b["msg"])
             ber_k.append(e)
             ck ^= int(np.bitwise_xor.reduce(out_h.view(np.uint32)))
@@ -626,9 +633,9 @@ def main():
             pmc = pmcs.get(b["name"], {})
             stages = stages_per_launch(b["opt"], b["input_num"])
             return {"kernel": b["name"] + ": " + vitdec.kernel_name(b["opt"]), "ms": round(kms[i], 4),
-                    "launch_ms": round(launch_ms[i], 4), "batches_per_launch": K,
+                    "launch_ms": round(launch_ms[i], 4), "batches_per_launch": P, "launches": len(sizes),
                     "achieved": round(ach, 2), "frac": round(ach / HBM_PEAK_GBS, 5),
-                    "algorithmic_bytes_per_batch": alg, "algorithmic_bytes_per_launch": alg * K,
+                    "algorithmic_bytes_per_batch": alg, "algorithmic_bytes_per_step_launches": alg * K,
                     "traffic": pmc.get("traffic_bytes"),
                     "valu": valu_view(pmc, kms[i], stages, b["name"], b["msg"])}
 
@@ -656,10 +663,11 @@ def main():
                 "n_bits_per_batch": N_BITS,
                 "decoded_bits_per_batch": batches[0]["msg"],
                 "parallelism": f"batch-shard x{world}" if world > 1 else "single GPU",
-                "launch": {"entry": "vd_run_device_batch", "batches_per_launch": K,
+                "launch": {"entry": "vd_run_device_batch", "batches_per_launch": P, "launches": len(sizes),
                            "what": "each workload's K steps as one launch of K independent batches (K "
-                                   "resident inputs from distinct seeds, K outputs, every batch's BER checked "
-                                   "against its source bits); kernel_ms is per batch = launch time / K",
+                                   "resident inputs from distinct seeds, every batch's BER checked against its "
+                                   "source bits; K > 128: launches of 128 resident batches, step k decoding "
+                                   "batch k % 128); kernel_ms is per batch = launch time / K",
                            "launch_ms": {b["name"]: round(t, 4) for b, t in zip(batches, launch_ms)},
                            "input_bytes_resident": {b["name"]: b["inps"].numel() for b in batches}},
                 "kernel_ms": {b["name"]: round(k, 4) for b, k in zip(batches, kms)},
