@@ -387,7 +387,9 @@ struct TgIn<SOFT16> {  // 1 stage per word: high 16 bits s0, low 16 bits s1
 };
 template <>
 struct TgIn<FP32> {  // 2 floats per stage, clamped to [-8,7]; BM = (int)(+-x0 +- x1) (truncation)
-    static constexpr bool FAB = false;  // ab() gives ints
+    // abf(): (A, B) as floats, truncated in fp32 (v_trunc_f32: one op where int conversion and back take
+    // two).  trunc gives -0 where (float)(int) gives +0, which the table's fma(A, 2^S, tag) cannot see.
+    static constexpr bool FAB = true;
     using raw_t = float2;
     static constexpr int RB = 256;
     static __device__ __forceinline__ uint64_t bytes(uint64_t stages) { return stages * 8; }
@@ -404,6 +406,12 @@ struct TgIn<FP32> {  // 2 floats per stage, clamped to [-8,7]; BM = (int)(+-x0 +
         const float x0 = fminf(fmaxf(v.x, -8.0f), 7.0f), x1 = fminf(fmaxf(v.y, -8.0f), 7.0f);
         A = (int)__fadd_rn(x0, x1);
         B = (int)__fsub_rn(x0, x1);
+    }
+    static __device__ __forceinline__ void abf(raw_t v, int, float& A, float& B, float)
+    {
+        const float x0 = fminf(fmaxf(v.x, -8.0f), 7.0f), x1 = fminf(fmaxf(v.y, -8.0f), 7.0f);
+        A = __builtin_truncf(__fadd_rn(x0, x1));
+        B = __builtin_truncf(__fsub_rn(x0, x1));
     }
 };
 template <class T, class = void>
