@@ -755,7 +755,9 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu((AB
                 // into byte / half g of the block's ring word (SDWA dst_sel: one op for shift and merge), then
                 // the field is cleared to 2^(S-1).  At the end of every block (32 stages) the decision-neutral
                 // renormalisation by the metric of position 0 follows: readfirstlane (1 wait state after the
-                // clear), the offset on the scalar unit, one vector subtract.
+                // clear), the offset on the scalar unit, one vector subtract.  s_sub_u32 writes SCC: the
+                // statements with VD_TG_RN declare it clobbered (without that, a compiler that keeps a branch
+                // condition in SCC across them decodes wrong words: the loop-wrapped study kernel did).
                 constexpr int g = (i % 32) / J;
                 uint32_t sr;
 #define VD_TG_RO(SEL, UNUSED) "v_lshrrev_b32_sdwa %[w], 1, %[V] dst_sel:" SEL " dst_unused:" UNUSED             \
@@ -765,19 +767,19 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu((AB
                 if constexpr (J == 8 && g == 0)
                     asm(VD_TG_RO("BYTE_0", "UNUSED_PAD") : [V] "+{v60}"(V), [w] "=&v"(word) : VD_TG_IN);
                 else if constexpr (J == 8 && g == 1 && RN16)
-                    asm(VD_TG_RO("BYTE_1", "UNUSED_PRESERVE") VD_TG_RN : [V] "+{v60}"(V), [w] "+v"(word), [sr] "=&s"(sr) : VD_TG_IN);
+                    asm(VD_TG_RO("BYTE_1", "UNUSED_PRESERVE") VD_TG_RN : [V] "+{v60}"(V), [w] "+v"(word), [sr] "=&s"(sr) : VD_TG_IN : "scc");
                 else if constexpr (J == 8 && g == 1)
                     asm(VD_TG_RO("BYTE_1", "UNUSED_PRESERVE") : [V] "+{v60}"(V), [w] "+v"(word) : VD_TG_IN);
                 else if constexpr (J == 8 && g == 2)
                     asm(VD_TG_RO("BYTE_2", "UNUSED_PRESERVE") : [V] "+{v60}"(V), [w] "+v"(word) : VD_TG_IN);
                 else if constexpr (J == 8)
-                    asm(VD_TG_RO("BYTE_3", "UNUSED_PRESERVE") VD_TG_RN : [V] "+{v60}"(V), [w] "+v"(word), [sr] "=&s"(sr) : VD_TG_IN);
+                    asm(VD_TG_RO("BYTE_3", "UNUSED_PRESERVE") VD_TG_RN : [V] "+{v60}"(V), [w] "+v"(word), [sr] "=&s"(sr) : VD_TG_IN : "scc");
                 else if constexpr (g == 0 && RN16)
-                    asm(VD_TG_RO("WORD_0", "UNUSED_PAD") VD_TG_RN : [V] "+{v60}"(V), [w] "=&v"(word), [sr] "=&s"(sr) : VD_TG_IN);
+                    asm(VD_TG_RO("WORD_0", "UNUSED_PAD") VD_TG_RN : [V] "+{v60}"(V), [w] "=&v"(word), [sr] "=&s"(sr) : VD_TG_IN : "scc");
                 else if constexpr (g == 0)
                     asm(VD_TG_RO("WORD_0", "UNUSED_PAD") : [V] "+{v60}"(V), [w] "=&v"(word) : VD_TG_IN);
                 else
-                    asm(VD_TG_RO("WORD_1", "UNUSED_PRESERVE") VD_TG_RN : [V] "+{v60}"(V), [w] "+v"(word), [sr] "=&s"(sr) : VD_TG_IN);
+                    asm(VD_TG_RO("WORD_1", "UNUSED_PRESERVE") VD_TG_RN : [V] "+{v60}"(V), [w] "+v"(word), [sr] "=&s"(sr) : VD_TG_IN : "scc");
 #undef VD_TG_IN
 #undef VD_TG_RN
 #undef VD_TG_RO
