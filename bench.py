@@ -78,7 +78,9 @@ def cpu_baseline(batches):
         match = match and bool(np.array_equal(out, gpu))
     all_cores = {"value": round(bits / dt_mt / 1e9, 6), "unit": "Gb/s", "cores": nt,
                  "sample": f"the same step on {nt} host threads (chunks split across threads) in {dt_mt:.2f} s"}
-    return {"value": round(bits / dt / 1e9, 6), "unit": "Gb/s", "cores": 1, "kind": "port", "cpu_model": cpu_model(),
+    return {"value": round(bits / dt / 1e9, 6), "unit": "Gb/s", "cores": 1, "kind": "port",
+            "what": "naive scalar restatement (oracle): the reference's decode semantics as a plain int64 "
+                    "64-state loop per chunk, not an optimised CPU decoder", "cpu_model": cpu_model(),
             "sample": f"one full bench step ({names}, 2 x 32M-bit batches, 6400-chunk partition) decoded by "
                       f"oracle/vd_oracle.c on 1 host thread in {dt:.1f} s; output identical to the GPU's: {match}",
             "matches_gpu": match, "all_cores": all_cores}
@@ -136,10 +138,6 @@ def valu_view(pmc, kernel_ms, stages, name, msg_bits):
     time and clock come from the same dispatches):
       cycles       = GRBM_GUI_ACTIVE / 8 XCDs                        (engine cycles of one dispatch)
       clock        = cycles / that run's kernel time
-      busy_pct     = 100 * SQ_ACTIVE_INST_VALU * 4 / (1024 SIMDs * cycles)
-                     (the gfx94x VALUBusy formula rocprofv3 falls back to on gfx950; it charges 4 cycles
-                     per wave64 VALU instruction, a SIMD-16 model, so it reads above 100 on the 32-lane
-                     gfx950 SIMD when every SIMD issues VALU back to back)
       issue_pct    = 100 * SQ_INSTS_VALU * 2 / (1024 * cycles)
                      (SIMD-32 model: a wave64 VALU instruction occupies its SIMD for 2 cycles at the
                      least; max/DPP/permlane/bit-field forms take 4 -- profiles/r02/ubench12.log)
@@ -159,8 +157,6 @@ def valu_view(pmc, kernel_ms, stages, name, msg_bits):
     if "GRBM_GUI_ACTIVE" in c:
         cyc = c["GRBM_GUI_ACTIVE"] / N_XCD
         v["issue_pct"] = round(100.0 * insts * 2 / (N_SIMD * cyc), 1)
-        if "SQ_ACTIVE_INST_VALU" in c:
-            v["busy_pct"] = round(100.0 * c["SQ_ACTIVE_INST_VALU"] * 4 / (N_SIMD * cyc), 1)
         v["cycles_per_inst_per_simd"] = round(N_SIMD * cyc / insts, 3)
         ghz = pmc.get("pmc_run_clock_ghz")
         if ghz:
@@ -230,6 +226,27 @@ def aggregate_gbps(bits_per_step, world, steps, elapsed_s):
     return bits_per_step * world * steps / elapsed_s / 1e9
 
 
+def free_port():
+    """A free TCP port on the loopback interface (rendezvous of the process group)."""
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def init_ranks(world, local):
+    """The process group every run uses, N = 1 included, so the N = 1 point runs the same collectives as
+    N > 1 (barrier, max over ranks, checksum gather, final gather): RCCL (backend "nccl") bound to this
+    rank's GPU.  A plain `python bench.py` at N = 1 has no launcher environment; it becomes rank 0 of a
+    1-rank group with its own rendezvous on 127.0.0.1."""
+    if "MASTER_ADDR" not in os.environ or "WORLD_SIZE" not in os.environ:
+        assert world == 1
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(free_port()), RANK="0", WORLD_SIZE="1",
+                          LOCAL_RANK="0")
+    torch.cuda.set_device(local)
+    torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+
 def max_over_ranks(elapsed, dev):
     t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
@@ -237,7 +254,7 @@ def max_over_ranks(elapsed, dev):
 
 
 def gather_checksums(sums, dev, world):
-    """The only cross-rank traffic: per-rank XOR checksums of the decoded words (after timing)."""
+    """Per-rank XOR checksums of the decoded words (after timing), all_gather of a few int64s."""
     cs = torch.tensor(sums, dtype=torch.int64, device=dev)
     gathered = [torch.empty_like(cs) for _ in range(world)]
     torch.distributed.all_gather(gathered, cs)
@@ -246,26 +263,26 @@ def gather_checksums(sums, dev, world):
 
 def gather_outputs(outs, dev, world, rank):
     """The north_star's final gather: every rank's decoded words (uint8 tensors, equal sizes) collected
-    over RCCL (ncclAllGather, the collective bench already uses for its checksums; gloo on CPU in
-    tests/test_dist.py).  Outside the timed region.  Returns (ms, per-rank XOR checksums of what rank 0
-    received, None) on rank 0, (ms, None, None) elsewhere, or (None, None, error) on every rank when any
-    rank could not allocate its receive buffers: the ranks agree on that (all_reduce of an ok flag)
-    before anyone enters the collective, so no rank is left waiting in it."""
+    on rank 0 over RCCL (torch.distributed.gather to dst 0: rank 0 receives world x the words, the other
+    ranks only send theirs; gloo on CPU in tests/test_dist.py).  Outside the timed region.  Returns (ms,
+    per-rank XOR checksums of what rank 0 received, None) on rank 0, (ms, None, None) elsewhere, or (None,
+    None, error) on every rank when a rank could not build its buffers: the ranks agree on that
+    (all_reduce of an ok flag) before anyone enters the collective, so no rank is left waiting in it."""
     err = None
     try:
         flat = torch.cat([o.view(-1) for o in outs])
-        bufs = [torch.empty_like(flat) for _ in range(world)]
+        bufs = [torch.empty_like(flat) for _ in range(world)] if rank == 0 else None
     except Exception as e:  # e.g. torch.OutOfMemoryError on this rank only
         err = str(e)[:200]
     ok = torch.tensor([0 if err else 1], dtype=torch.int32, device=dev)
     torch.distributed.all_reduce(ok, op=torch.distributed.ReduceOp.MIN)
     if int(ok.item()) == 0:
-        return None, None, err or "a peer rank could not allocate its all_gather buffers"
+        return None, None, err or "a peer rank could not build its gather buffers"
     torch.distributed.barrier()
     if flat.is_cuda:
         torch.cuda.synchronize()
     t = time.perf_counter()
-    torch.distributed.all_gather(bufs, flat)
+    torch.distributed.gather(flat, gather_list=bufs, dst=0)
     if flat.is_cuda:
         torch.cuda.synchronize()
     ms = (time.perf_counter() - t) * 1e3
@@ -458,13 +475,9 @@ def launch_ranks(nproc, argv):
     """`bench.py --gpus N` (N > 1) without a torch.distributed launcher: start N ranks with
     torch.distributed.run as a CHILD process (this process has not touched the GPU and never will), pass
     its output through, and return its exit code.  Each rank re-enters main() with WORLD_SIZE set."""
-    import socket
     import subprocess
-    with socket.socket() as s:  # a free rendezvous port on the loopback interface
-        s.bind(("127.0.0.1", 0))
-        port = s.getsockname()[1]
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
-           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__), *argv]
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()), os.path.abspath(__file__), *argv]
     return subprocess.call(cmd)
 
 
@@ -508,13 +521,9 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if args.ranks_check:
         return ranks_check(world, rank)
-    if not args.ranks_check and torch.cuda.device_count() < world:
+    if torch.cuda.device_count() < world:
         sys.exit(f"bench.py: {world} ranks but only {torch.cuda.device_count()} visible GPU(s)")
-    if world > 1:
-        torch.cuda.set_device(local)
-        torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local))
-    else:
-        torch.cuda.set_device(0)
+    init_ranks(world, local)
     dev = torch.cuda.current_device()
     stream = torch.cuda.current_stream()
     sptr = stream.cuda_stream
@@ -565,8 +574,7 @@ def main():
             run(b)
         nwarm += K
         torch.cuda.synchronize()
-    if world > 1:
-        torch.distributed.barrier()
+    torch.distributed.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     evs[0].record(stream)
@@ -574,25 +582,27 @@ def main():
         run(b)
         evs[i + 1].record(stream)
     torch.cuda.synchronize()
-    if world > 1:
-        torch.distributed.barrier()
+    torch.distributed.barrier()
     elapsed = time.perf_counter() - t0
 
     # per-launch durations from the HIP events on the launch stream; per batch = / K
     launch_ms = [evs[i].elapsed_time(evs[i + 1]) for i in range(nw)]
     kms = [t / K for t in launch_ms]
     # correctness side-channel (outside the timed region): the decoded-bit error rate of every batch
-    # against its own source bits (max over the resident batches), and an RCCL all_gather of per-rank
-    # checksums of the decoded words (xor over each batch's words, xor over the batches: the only
-    # cross-GPU traffic)
+    # against its own source bits (max over the resident batches), and per-rank checksums of the decoded
+    # words: per workload the xor over every resident batch's words, then the xor of batch 0's words (the
+    # batch the final gather collects, which checks what rank 0 received against them)
     bers = []
-    sums = []
+    sums, sums0 = [], []
     for b in batches:
         ber_k, ck = [], 0
         for k in range(P):
             e, out_h = batch_ber(b["opt"], b["bits"], b["outs"], b["ostride"], b["nout"], k, b["msg"])
             ber_k.append(e)
-            ck ^= int(np.bitwise_xor.reduce(out_h.view(np.uint32)))
+            x = int(np.bitwise_xor.reduce(out_h.view(np.uint32)))
+            ck ^= x
+            if k == 0:
+                sums0.append(x)
         bers.append(max(ber_k))
         sums.append(ck)
     llr = None if (args.no_llr or rank != 0) else llr_side_measurement(dev, sptr, stream)
@@ -600,22 +610,21 @@ def main():
     chan = None if (args.no_channel or rank != 0) else channel_side_measurement(dev, sptr)
     other = None if (args.no_other or rank != 0) else other_configs_side_measurement(dev, sptr, stream)
     single = None if (args.no_other or rank != 0) else single_launch_side_measurement(batches, stream, sptr)
+    # the same collectives at every N (N = 1: a 1-rank RCCL group)
+    elapsed = max_over_ranks(elapsed, dev)
+    gathered = gather_checksums(sums + sums0, dev, world)
+    gms, gsums, err = gather_outputs([b["out"] for b in batches], dev, world, rank)
     final_gather = None
-    if world > 1:
-        elapsed = max_over_ranks(elapsed, dev)
-        gathered = gather_checksums(sums, dev, world)
-        gms, gsums, err = gather_outputs([b["out"] for b in batches], dev, world, rank)
-        if rank == 0:
-            if err is not None:  # a side measurement: report it, keep the bench line
-                final_gather = {"error": err}
-            else:
-                nbytes = sum(b["out"].numel() for b in batches)
-                final_gather = {"what": "every rank's decoded words collected over RCCL (all_gather)",
-                                "bytes_per_rank": nbytes, "ms": round(gms, 3),
-                                "GBps_into_each_rank": round(nbytes * (world - 1) / (gms * 1e-3) / 1e9, 2),
-                                "checksums_match": gsums == gathered}
-    else:
-        gathered = [sums]
+    if rank == 0:
+        if err is not None:  # a side measurement: report it, keep the bench line
+            final_gather = {"error": err}
+        else:
+            nbytes = sum(b["out"].numel() for b in batches)
+            final_gather = {"what": "every rank's decoded words (batch 0 of each workload) gathered on rank 0 "
+                                    "over RCCL (torch.distributed.gather, dst 0)",
+                            "bytes_per_rank": nbytes, "world": world, "ms": round(gms, 3),
+                            "GBps_into_rank0": round(nbytes * (world - 1) / (gms * 1e-3) / 1e9, 2),
+                            "checksums_match": gsums == [g[nw:] for g in gathered]}
 
     if rank == 0:
         bits_per_step = sum(b["msg"] for b in batches)
@@ -662,7 +671,7 @@ def main():
                             "reference's 6400-chunk partition",
                 "n_bits_per_batch": N_BITS,
                 "decoded_bits_per_batch": batches[0]["msg"],
-                "parallelism": f"batch-shard x{world}" if world > 1 else "single GPU",
+                "parallelism": f"batch-shard x{world}" if world > 1 else "single GPU (1-rank RCCL group)",
                 "launch": {"entry": "vd_run_device_batch", "batches_per_launch": P, "launches": len(sizes),
                            "what": "each workload's K steps as one launch of K independent batches (K "
                                    "resident inputs from distinct seeds, every batch's BER checked against its "
@@ -703,7 +712,8 @@ def main():
                 },
                 "per_kernel": {b["name"]: rl[i] for i, b in enumerate(batches)},
             },
-            "checksums": [[hex(x) for x in g] for g in gathered],
+            "checksums": [[hex(x) for x in g[:nw]] for g in gathered],
+            "checksums_are": "per rank, per workload: xor of the decoded words over every resident batch",
         }
         if llr is not None:
             result["config"]["llr_input"] = llr
@@ -723,8 +733,7 @@ def main():
 
     for b in batches:
         b["dec"].close()
-    if world > 1:
-        torch.distributed.destroy_process_group()
+    torch.distributed.destroy_process_group()
 
 
 if __name__ == "__main__":

@@ -182,6 +182,7 @@ struct vd_decoder {
     hipStream_t s_in = nullptr, s_out = nullptr;
     DeviceState* ds = nullptr;  // the device's board / split state (looked up once, vd_create)
     bool split = true;          // split launches allowed (VD_NO_SPLIT=1 at vd_create: no)
+    uint32_t* check = nullptr;  // LDS guard violation counter (vd_set_guard_check), null = off
 };
 
 static int ensure_capacity(vd_decoder* d, size_t inBytes, size_t outBytes)
@@ -207,20 +208,13 @@ static int ensure_capacity(vd_decoder* d, size_t inBytes, size_t outBytes)
 //  * the progress board of the decode kernels' fairness controller (vd_kernels.h Fair, Geom::fair),
 //    every word kFairEmpty at rest (the kernels free their slots); concurrent launches sharing it only
 //    perturb issue priorities;
-//  * the boundary vectors of split launches (vd_kernel_tg.h "split chunks"): kSplitSlots slots, a launch
-//    takes the next one, so up to kSplitSlots split launches may run on a device at once (far more than
-//    the hardware queues a process gets);
-//  * the re-decode counter (vd_split_redecodes).
-// A decoder looks it up once (vd_create), not per launch.
-constexpr int kSplitSlots = 32;
-constexpr int kSpecVecs = vd::kSplitVecs;  // per split chunk
+//  * the re-decode counter of split launches (vd_split_redecodes).
+// Split launches keep their boundary vectors in LDS (vd_kernel_tg.h "split chunks"), so launches on any
+// number of streams share no scratch.  A decoder looks the state up once (vd_create), not per launch.
 struct DeviceState {
     uint32_t* board = nullptr;
     int nsimd = 0;
-    uint32_t maxSplit = 0;  // split chunks a slot holds
-    float* spec = nullptr;  // [slot][maxSplit][kSpecVecs][64]
     uint32_t* stats = nullptr;
-    std::atomic<uint32_t> next{0};
 };
 static DeviceState* device_state(int device)
 {
@@ -234,12 +228,10 @@ static DeviceState* device_state(int device)
             return nullptr;
         DeviceState* x = new DeviceState;
         x->nsimd = 4 * cus;
-        x->maxSplit = (uint32_t)(x->nsimd / vd::kWaves);
-        const size_t nspec = (size_t)kSplitSlots * x->maxSplit * kSpecVecs * 64;
         if (hipMalloc(&x->board, vd::kFairBoardWords * 4) != hipSuccess ||
             hipMemset(x->board, 0xFF, vd::kFairBoardWords * 4) != hipSuccess ||
-            hipMalloc(&x->spec, nspec * 4) != hipSuccess || hipMalloc(&x->stats, 4) != hipSuccess ||
-            hipMemset(x->stats, 0, 4) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
+            hipMalloc(&x->stats, 4) != hipSuccess || hipMemset(x->stats, 0, 4) != hipSuccess ||
+            hipDeviceSynchronize() != hipSuccess) {
             delete x;
             return nullptr;
         }
@@ -249,16 +241,14 @@ static DeviceState* device_state(int device)
 }
 // Split the launch when the whole chunks leave exactly one piece wave per SIMD (6400 chunks on 1024
 // SIMDs: 6 whole chunks per SIMD + 256 chunks in 4 pieces) and the chunks are long enough.
-static void plan_split(vd::Geom& g, int options, DeviceState* x)
+static void plan_split(vd::Geom& g, int options, const DeviceState* x)
 {
     const uint64_t words32 = out_of(options) != 0 ? g.packNum / 2 : g.packNum;  // O_B16: 16-bit words
     if (words32 / g.nchunks < (uint64_t)vd::kSplitMinWords) return;
     const uint32_t nsimd = (uint32_t)x->nsimd;
     const uint32_t perSimd = g.nchunks / nsimd, rem = g.nchunks % nsimd, nwhole = g.nchunks - rem;
-    if (rem == 0 || rem * vd::kWaves != nsimd || perSimd + 1 > 8) return;  // 8 waves per SIMD (vd_kernel_tg.h TgRing)
-    const uint32_t slot = x->next.fetch_add(1) % kSplitSlots;
+    if (rem == 0 || rem * vd::kWaves != nsimd || perSimd + 1 > 8) return;  // 8 waves per SIMD (vd_kernel_tg.h kTbs)
     g.nwhole = nwhole;
-    g.spec = x->spec + (size_t)slot * x->maxSplit * kSpecVecs * 64;
     g.stats = x->stats;
 }
 
@@ -278,7 +268,16 @@ static int launch_decode(const vd_decoder* d, const void* in_d, void* out_d, siz
     g.nchunks = vd::kChunks;
     g.scale = scale;
     if (g.packNum == 0) return VD_OK;
+    // the launch goes to the stream's device (the null stream: the current device); the board and the
+    // guard counter belong to the decoder's device
+    int sdev = -1;
+    if (s) VD_HIP(hipStreamGetDevice(s, &sdev));
+    else VD_HIP(hipGetDevice(&sdev));
+    if (sdev != d->device)
+        return fail(VD_ERR_ARG, "stream on device " + std::to_string(sdev) + ", decoder on device " +
+                                    std::to_string(d->device));
     g.fair = d->ds->board;
+    g.check = d->check;
     g.nbatch = nbatch;
     g.inStride = inStride;
     g.outStride = outStride;
@@ -335,6 +334,11 @@ int vd_create(int options, size_t preallocInputNum, int device, vd_decoder** out
     }
     const char* nosplit = std::getenv("VD_NO_SPLIT");
     d->split = !(nosplit && nosplit[0] == '1');
+    const char* chk = std::getenv("VD_CHECK");
+    if (chk && chk[0] == '1') {
+        int rc = vd_set_guard_check(d, 1);
+        if (rc != VD_OK) { vd_destroy(d); return rc; }
+    }
     if (hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreate(&d->ev0) != hipSuccess || hipEventCreate(&d->ev1) != hipSuccess) {
         vd_destroy(d);
@@ -363,6 +367,7 @@ int vd_destroy(vd_decoder* d)
     if (d->ev0) (void)hipEventDestroy(d->ev0);
     if (d->ev1) (void)hipEventDestroy(d->ev1);
     if (d->stream) (void)hipStreamDestroy(d->stream);
+    if (d->check) (void)hipFree(d->check);
     delete d;
     return VD_OK;
 }
@@ -394,6 +399,34 @@ int vd_run(vd_decoder* d, const void* input_h, void* output_h, size_t inputNum, 
     VD_HIP(hipMemcpyAsync(output_h, d->out_d, outB, hipMemcpyDeviceToHost, d->stream));
     VD_HIP(hipStreamSynchronize(d->stream));
     if (kernel_ms) VD_HIP(hipEventElapsedTime(kernel_ms, d->ev0, d->ev1));
+    return VD_OK;
+}
+
+int vd_set_guard_check(vd_decoder* d, int enable)
+{
+    if (!d) return fail(VD_ERR_ARG, "null argument");
+    VD_HIP(hipSetDevice(d->device));
+    if (!enable) {
+        if (d->check) VD_HIP(hipDeviceSynchronize());
+        if (d->check) (void)hipFree(d->check);
+        d->check = nullptr;
+        return VD_OK;
+    }
+    if (!d->check) VD_HIP(hipMalloc(&d->check, 4));
+    VD_HIP(hipMemset(d->check, 0, 4));
+    VD_HIP(hipDeviceSynchronize());
+    return VD_OK;
+}
+
+int vd_guard_violations(vd_decoder* d, uint64_t* count)
+{
+    if (!d || !count) return fail(VD_ERR_ARG, "null argument");
+    if (!d->check) return fail(VD_ERR_ARG, "guard check not enabled (vd_set_guard_check)");
+    VD_HIP(hipSetDevice(d->device));
+    VD_HIP(hipDeviceSynchronize());
+    uint32_t v = 0;
+    VD_HIP(hipMemcpy(&v, d->check, 4, hipMemcpyDeviceToHost));
+    *count = v;
     return VD_OK;
 }
 

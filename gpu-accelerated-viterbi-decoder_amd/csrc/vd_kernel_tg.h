@@ -1,32 +1,35 @@
-// vd_kernel_tg.h -- "tagged" decode kernel vd_decode_tg (gfx950): the survivor decision of every stage
-// rides in the low bits of the fp32 path metric, so one add-compare-select is three VALU ops
-// (add, DPP-fused sub, max) instead of five, and two of the six butterfly distances move from LDS
-// permutes to VALU permlane swaps.  Same decode semantics as vd_decode_sc (reference hot path
-// src/viterbi/viterbi.cu:144-207, viterbiACS.cuh:113-157,216-256, viterbiTB.cuh:4-21): bit-exact for
-// every valid option except SOFT16, whose branch metrics (|BM| up to 65534) leave no room for the tags.
+// vd_kernel_tg.h -- the decode kernel vd_decode_tg<CH, CORE, OB> (gfx950), one instantiation per input
+// format x metric core x output width.  Reference hot path: viterbi_core (src/viterbi/viterbi.cu:144-207)
+// with viterbiBM.cuh (branch metrics), viterbiACS.cuh:113-157,216-256 (ACS and tie rules) and
+// viterbiTB.cuh:4-21 (traceback); bit-exact with it for every valid option.
 //
-// Metric word.  V = metric * 2^S + h, an exact integer in fp32 (|V| < 2^24).  At stage j of a J-stage
-// history field (S = J+1), the own candidate gets tag +c*2^j and the exchanged one -c*2^j, c = +1 where
-// the reference's tie rule lets the own predecessor win ties, -1 where the exchanged one does:
+// Tagged ACS: the survivor decision of every stage rides in the low bits of the path metric.  A metric
+// word is V = metric * 2^S + h, an exact integer in fp32 (|V| < 2^24).  At stage j of a J-stage history
+// field (S = J+1), the own candidate gets tag +c*2^j and the exchanged one -c*2^j, c = +1 where the
+// reference's tie rule lets the own predecessor win ties, -1 where the exchanged one does:
 //   t1 = V_own + (BM*2^S + c*2^j),  t2 = V_exch - (BM*2^S + c*2^j),  V' = max(t1, t2).
-// The history h = sum of the chosen signed digits (+-2^i, i < j) satisfies |h| < 2^j, so on equal
-// metrics the tag decides (the tie rule), and on unequal metrics (a difference of >= 2^S) neither tags
-// nor history can flip the order: every decision equals the reference's int32/int16/fp16 decision.
-// V is kept in [2^23, 2^24) (offset 1.25*2^23), where the fp32 ulp is 1 and the low mantissa bits are
-// the low integer bits, and each field starts at 2^(S-1): after J stages the field 2^(S-1) + h is in
-// (0, 2^S), its decision bits (h + 2^J - 1) / 2 are mantissa bits 1..J, and clearing it is one
-// v_and_or_b32.  Renormalising at the end of every 32-stage block keeps V in range (bounds below).
+// The history h = sum of the chosen signed digits (+-2^i, i < j) satisfies |h| < 2^j, so on equal metrics
+// the tag decides (the tie rule), and on unequal metrics (a difference of >= 2^S) neither tags nor history
+// can flip the order: every decision equals the reference's int32/int16/fp16 decision, and the max copies
+// the winner's history into the lane (a register exchange within the field).  V is kept in [2^23, 2^24)
+// (base 1.25*2^23), where the fp32 ulp is 1 and the low mantissa bits are the low integer bits, and every
+// field starts at 2^(S-1): after J stages the field 2^(S-1) + h is in (0, 2^S), its decision bits
+// (h + 2^J - 1) / 2 are mantissa bits 1..J, and clearing it is one v_and_or_b32.  Renormalising at the end
+// of every 32-stage block keeps V in range (bounds below).
 //
 // SOFT16 (|BM| up to 65536: a metric spread near 2^21) leaves no room for the tags below 2^24, so its
-// kernel runs the same scheme on int32 patterns (TgFmt::INT): V = metric * 2^S + 2^(S-1) + h with |V| <
-// 2^30, integer add / DPP subtract / signed max, and the same bit-field read-out.
+// kernel runs the same scheme on int32 patterns (TgFmt::INT): V = metric * 2^S + 2^(S-1) + h with
+// |V| < 2^31, integer add / DPP subtract / signed max, and the same bit-field read-out.
 //
-// Lane encoding.  Position p (the trellis state rotr6(p, t%6) after stage t, as in vd_decode_sc) lives
-// in lane l = p0*1 ^ p1*2 ^ p2*7 ^ p3*8 ^ p4*16 ^ p5*32, so the butterfly partner p ^ (1<<q) is lane
-// l ^ {1, 2, 7, 8, 16, 32}[q]: DPP quad_perm (xor 1, 2), row_half_mirror (xor 7), row_ror:8 (xor 8)
-// -- each fused into the sub -- and v_permlane16_swap / v_permlane32_swap (xor 16, 32).  A swap stage
-// forms a = V + X, b = V + Y in every lane and swaps halves, after which each lane holds its own and
-// its exchanged candidate (X, Y = +-M of the lane and of its partner, from the branch-metric table).
+// Lane encoding.  Position p holds after stage t the trellis state rotr6(p, t%6); p lives in lane
+// l = p0*1 ^ p1*2 ^ p2*7 ^ p3*8 ^ p4*16 ^ p5*32, so the butterfly partner p ^ (1<<q), q = (t%6+5)%6, is
+// lane l ^ {1, 2, 7, 8, 16, 32}[q]: DPP quad_perm (xor 1, 2), row_half_mirror (xor 7) and row_ror:8
+// (xor 8), each fused into the max; ds_swizzle (xor 16) and ds_bpermute (xor 32) fetch the partner's
+// metric through the LDS crossbar (no memory access).
+//
+// LDS per wave: [guard | branch-metric table | guard | survivor ring | guard].  The guard words are
+// written and checked only when Geom::check is set (tests: any out-of-bounds LDS store of the table or
+// ring lands in a guard and is counted at kernel exit).
 #pragma once
 #include <type_traits>
 #include "vd_kernels.h"
@@ -37,19 +40,17 @@ namespace vd {
 // channel ids: HARD..FP32 = packed input (viterbiBM.cuh formats); 8 + base = float channel values
 // quantised on the fly exactly like SoftDecisionPacker(base, scale) would have packed them (vd_pack.h)
 constexpr int kLlr = 8;
-// I16 (ABL bit 26, tools): SOFT4 / SOFT8 / FP32 on int32 patterns with 16-stage fields (S = 17): half the
-// field read-outs and traceback reads of J = 8; 7168 * 2^17 < 2^30 keeps |V +- E| < 2^31.
-constexpr int kAblI16 = 1 << 26;
-constexpr int kAblRn16 = 1 << 27;     // tools: renormalisation every 16 stages around 1.5*2^23
-constexpr int kAblNoS01 = 1 << 30;    // tools: SOFT8 table rows from (A, B) instead of the two soft values
-constexpr int kAblFairAll = 1 << 29;  // tools: fairness controller on every batch of a batched launch
-constexpr int kAbl7w = 1 << 28;   // tools: 13 ring slots per wave, 7 waves per SIMD (before r02's last commits)
-template <int CH, int ABL = 0>
+// Component ablations (tools/vd_ablate only; the outputs are wrong): the template argument ABL of
+// vd_decode_tg is a set of these bits, 0 in the product.
+constexpr int kAblNoTraceback = 1, kAblNoTabReads = 2, kAblNoReadout = 4, kAblNoTabBuild = 8, kAblNoLoads = 16,
+              kAblClock = 32, kAblNoFair = 256, kAblNoTabWrites = 512, kAblNoGuardSpace = 1024;
+constexpr int kAblAcsOnly = kAblNoTraceback | kAblNoTabReads | kAblNoReadout | kAblNoTabBuild | kAblNoLoads;
+
+template <int CH>
 struct TgFmt {
-    static constexpr bool I16 = (ABL & kAblI16) && (CH & 7) != HARD && (CH & 7) != SOFT16;
-    static constexpr bool INT = (CH & 7) == SOFT16 || I16;         // int32 metric patterns instead of fp32
-    static constexpr int J = (CH & 7) == HARD || I16 ? 16 : 8;     // stages per history field
-    static constexpr int S = J + 1;                                // metric scale 2^S
+    static constexpr bool INT = (CH & 7) == SOFT16;       // int32 metric patterns instead of fp32
+    static constexpr int J = (CH & 7) == HARD ? 16 : 8;   // stages per history field
+    static constexpr int S = J + 1;                       // metric scale 2^S
 };
 // Range.  The largest path metric never decreases (the best state's two successors get +-x, one of
 // them >= it) and grows by at most BMmax per stage; every metric lies within D = (K-1)*(BMmax-BMmin) of
@@ -62,24 +63,22 @@ struct TgFmt {
 //   SOFT4/FP32 (BMmax 16):  [-209, 192+512+17] fits.
 // SOFT16 (int32, base 0, BMmax 65536, 2^9 units, 2^22 each way): [-851,969, 786,432+2,097,152+65,537]
 // fits, so |V +- E| < 2^31.  The CLI default SNR 15 (saturated soft values on the codeword: the best
-// path gains BMmax every stage) is in the parity tests.  (Until r02's last commits: renormalisation every 16 stages around 1.5*2^23.)
+// path gains BMmax every stage) is in the parity tests; tests/test_metric_range.py checks the bounds.
 
-// branch-metric table: per 96-stage group, 16 periods of 6 rows (row K = stage phase); a row holds
-// BM[L]*2^S + c*2^j for the four labels L.  M_B32 rows of phase 0 hold a second set with the other
-// tag sign (its tie rule differs between position halves there).  Rows K of periods 2m and 2m+1 are
-// interleaved entry by entry, so a lane's entries for stages t and t+6 are one 8-byte ds_read_b64:
-// entry e of row r sits at row(r) + 8e.
-template <int CORE>
+// Branch-metric table: per 96-stage group, 16 periods of 6 rows (row K = stage phase); a row holds
+// E[L] = BM[L]*2^S + tag for the four labels L.  Rows K of periods 2m and 2m+1 are interleaved entry by
+// entry, so a lane's entries for stages t and t+6 are one 8-byte ds_read_b64: entry e of row r sits at
+// row(r) + 8e.  The SOFT16 (INT, M_B32) phase-0 rows hold, per label, the pair (E-, E+) of both tag
+// signs (the M_B32 tie rule differs between the position halves there, viterbiACS.cuh:137-142); the fp32
+// cores take M_B32's upper-half phase-0 entries from the ordinary row instead (S32 in the kernel).
+template <bool PAIR0>
 struct TgTab {
-    // M_B32's phase-0 rows hold, per label and period, the pair (E-, E+) of both tag signs (its tie
-    // rule differs between the position halves there); every other row holds E[L] for the four labels
-    // with periods 2m, 2m+1 interleaved, so one ds_read_b64 serves a stage and the stage 6 later.
-    static __host__ __device__ constexpr bool pairrow(int K) { return CORE == B32 && K == 0; }
-    // dword offsets: period pair m at 60m, row K at ks(K) (8 dwords, M_B32's phase-0 row 16), padded so
-    // the 32-lane stores of a table build hit (nearly) distinct banks
+    static __host__ __device__ constexpr bool pairrow(int K) { return PAIR0 && K == 0; }
+    // dword offsets: period pair m at 60m, row K at ks(K) (8 dwords, a pair row 16), padded so the
+    // 32-lane stores of a table build hit (nearly) distinct banks
     static __host__ __device__ constexpr int ks(int K)
     {
-        return CORE == B32 ? (K == 0 ? 0 : K == 1 ? 18 : K == 2 ? 26 : K == 3 ? 34 : K == 4 ? 44 : 52) : 10 * K;
+        return PAIR0 ? (K == 0 ? 0 : K == 1 ? 18 : K == 2 ? 26 : K == 3 ? 34 : K == 4 ? 44 : 52) : 10 * K;
     }
     static __host__ __device__ constexpr int row(int r)
     {
@@ -87,13 +86,27 @@ struct TgTab {
     }
     static constexpr int BYTES = 8 * 60 * 4;
 };
-// survivor ring slots per wave: table + ring of 4 waves fit 8 workgroups per CU (19,968 B each), so every
-// SIMD holds 8 waves (61 VGPRs): 1.4 % faster per batch than 13 slots at 7 waves under bench conditions
-// (profiles/r02/benchab_8w.log), the shorter traceback batches included
-template <int CORE>
-struct TgRing {
-    static constexpr int TBS = 11;
+// Survivor ring slots per wave minus one (words traced per traceback batch): table + ring + guards of 4
+// waves (20,160 B) fit 8 workgroups per CU, so every SIMD holds 8 waves (<= 64 VGPRs): 1.4 % faster per
+// batch than 13 slots at 7 waves (profiles/r02/benchab_8w.log), the shorter traceback batches included.
+constexpr int kTbs = 11;
+constexpr int kGuardWords = 4;                 // guard words before the table, between table and ring, after the ring
+constexpr uint32_t kGuardPattern = 0xA5C3E10Fu;
+template <bool PAIR0, int GW = kGuardWords>
+struct TgLds {
+    static constexpr int TAB = TgTab<PAIR0>::BYTES / 4;     // table words
+    static constexpr int RING = (kTbs + 1) * 64;           // ring words
+    static constexpr int TAB_OFF = GW;                     // word offsets within a wave's part
+    static constexpr int RING_OFF = 2 * GW + TAB;
+    static constexpr int WAVE = 3 * GW + TAB + RING;
+    // guard word i (0 .. 3 GW - 1) of a wave's part
+    static __device__ __forceinline__ int guard(int i)
+    {
+        return i < GW ? i : i < 2 * GW ? TAB + i : TAB + RING + i;
+    }
 };
+static_assert(kWaves * TgLds<false>::WAVE * 4 <= 20480 && kWaves * TgLds<true>::WAVE * 4 <= 20480,
+              "8 workgroups of 4 waves per CU (160 KiB of LDS)");
 
 __device__ __forceinline__ int tg_pos(int l)
 {
@@ -108,32 +121,17 @@ __host__ __device__ constexpr int tg_label(int p, int k)
     const int R = (T << 1) | (O & 1);
     return (tg_par7(R & 0171) << 1) | tg_par7(R & 0133);
 }
-// label flip of the butterfly partner in the two swap phases: 0 (checked at compile time)
-static_assert(tg_label(32, 0) == 0 && tg_label(16, 5) == 0, "swap partners share the label");
+// label flip of the butterfly partner in the two LDS-exchange phases: 0 (checked at compile time)
+static_assert(tg_label(32, 0) == 0 && tg_label(16, 5) == 0, "exchange partners share the label");
 
 // ---------------------------------------------------------------- stages (inline asm, exact op order)
-// The path metric V is pinned to v60 ("{v60}" constraints) so that the swap stage's packed FMA can
-// name the pair v[60:61] and read V for both of its halves (op_sel_hi 0); v62:v63 are its scratch.
+// The path metric V is pinned to v60 ("{v60}" constraints).
 typedef float f2v __attribute__((ext_vector_type(2)));
-// DPP stage, exchange lane xor {1,2,7,8}[Q].  The DPP source (V) is >= 2 VALU slots after its write.
-template <int Q>
-__device__ __forceinline__ void tg_stage_dpp(float& V, float m)
-{
-    float t1, t2;
-#define VD_TG_DPP(CTRL)                                                                                   \
-    asm("v_add_f32 %1, %0, %3\n\ts_nop 0\n\tv_sub_f32_dpp %2, %0, %3 " CTRL " row_mask:0xf bank_mask:0xf\n\t" \
-        "v_max_f32 %0, %1, %2"                                                                           \
-        : "+{v60}"(V), "=&v"(t1), "=&v"(t2) : "v"(m))
-    if constexpr (Q == 0) VD_TG_DPP("quad_perm:[1,0,3,2]");
-    else if constexpr (Q == 1) VD_TG_DPP("quad_perm:[2,3,0,1]");
-    else if constexpr (Q == 2) VD_TG_DPP("row_half_mirror");
-    else VD_TG_DPP("row_ror:8");
-#undef VD_TG_DPP
-}
-// DPP stage, two-op form: the butterfly partner has the same branch label and tag in every DPP phase,
-// so its V_exch - m is what this lane would compute from its own V: a = V + m, b = V - m, and the max
-// takes b from the partner through the DPP operand, V' = max(a, dpp(b)).  b is read by DPP 2 slots
-// after its write.
+// DPP stage, exchange lane xor {1,2,7,8}[Q].  The butterfly partner has the same branch label and tag
+// in every DPP phase, so its V_exch - m is what this lane would compute from its own V: a = V + m,
+// b = V - m, and the max takes b from the partner through the DPP operand, V' = max(a, dpp(b)).  b is
+// read by DPP 2 slots after its write.  (The three-op form v_add, v_sub_f32_dpp, v_max decides the same;
+// this one is 0.5-1 % faster, profiles/r02/benchab_dpp_forms_8w.log.)
 template <int Q>
 __device__ __forceinline__ void tg_stage_dpp2(float& V, float m)
 {
@@ -148,51 +146,34 @@ __device__ __forceinline__ void tg_stage_dpp2(float& V, float m)
     else VD_TG_DPP2("row_ror:8");
 #undef VD_TG_DPP2
 }
-// xor-32 swap stage (tools, ABL 8192): [a, b] = [m, m'] * [sx, -sx] + [V, V] in one v_pk_fma_f32, swap
-// halves across lanes, max.  The butterfly partner has the same label, so m' = m except in M_B32's
-// phase-0 rows (m, m' = the two tag signs).  SEL picks the halves of the table pair e: 0 = (lo, lo) (even
-// period), 1 = (hi, hi) (odd period), 2 = (lo, hi) (M_B32 phase 0).
-template <int SEL>
-__device__ __forceinline__ void tg_stage_swap(float& V, f2v e, f2v s)
-{
-#define VD_TG_SWAP(OS)                                                                                      \
-    asm("v_pk_fma_f32 v[62:63], %1, %2, v[60:61] " OS "\n\ts_nop 1\n\tv_permlane32_swap_b32 v62, v63\n\t"      \
-        "v_max_f32 %0, v62, v63"                                                                           \
-        : "+{v60}"(V) : "v"(e), "v"(s) : "v62", "v63")
-    if constexpr (SEL == 0) VD_TG_SWAP("op_sel:[0,0,0] op_sel_hi:[0,1,0]");
-    else if constexpr (SEL == 1) VD_TG_SWAP("op_sel:[1,0,0] op_sel_hi:[1,1,0]");
-    else VD_TG_SWAP("op_sel:[0,0,0] op_sel_hi:[1,1,0]");
-#undef VD_TG_SWAP
-}
 
-// swap stage with the partner's metric fetched through the LDS crossbar (ds_bpermute, no memory access)
-// instead of a VALU lane swap: V' = max(V + m, V_partner - m), the DPP stage's formula, with m the
-// entry of this lane's class (M_B32 phase 0: E- in the lower position half, E+ in the upper one).
+// LDS-exchange stage: the partner's metric vp through the LDS crossbar (ds_swizzle / ds_bpermute), then
+// V' = max(V + m, vp - m), the DPP stage's formula.  A VALU lane swap (v_permlane32_swap) costs about two
+// DPP ops of issue; this costs three plain ops and one LDS round trip (profiles/r02/ablate.log).
 __device__ __forceinline__ float tg_partner(float V, int paddr)
 {
     return __builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute(paddr, __builtin_bit_cast(int, V)));
 }
-// M_B32 phase-0 stage with the signed entry (S32 in the kernel): V' = max(V + s*m, V_partner - s*m)
-template <int SEL>
-__device__ __forceinline__ void tg_stage_lds_sg(float& V, f2v e, float vp, float sg)
+__device__ __forceinline__ float tg_swz16(float V)
 {
-    const float m = SEL == 0 ? e.x : e.y;
-    float t1, t2;
-    asm("v_fma_f32 %1, %3, %5, %0\n\tv_fma_f32 %2, -%3, %5, %4\n\tv_max_f32 %0, %1, %2"
-        : "+{v60}"(V), "=&v"(t1), "=&v"(t2) : "v"(m), "v"(vp), "v"(sg));
+    return __builtin_bit_cast(float, __builtin_amdgcn_ds_swizzle(__builtin_bit_cast(int, V), 0x401F));
 }
-template <int SEL>
-__device__ __forceinline__ void tg_stage_lds(float& V, f2v e, float vp, bool upper)
+__device__ __forceinline__ void tg_stage_lds(float& V, float m, float vp)
 {
-    const float m = SEL == 0 ? e.x : SEL == 1 ? e.y : (upper ? e.y : e.x);
     float t1, t2;
     asm("v_add_f32 %1, %0, %3\n\tv_sub_f32 %2, %4, %3\n\tv_max_f32 %0, %1, %2"
         : "+{v60}"(V), "=&v"(t1), "=&v"(t2) : "v"(m), "v"(vp));
 }
+// M_B32 phase-0 stage (S32): V' = max(V + s*m, vp - s*m), s = -1 in the upper position half, where m is
+// the entry of the complementary label (see the kernel)
+__device__ __forceinline__ void tg_stage_lds_sg(float& V, float m, float vp, float sg)
+{
+    float t1, t2;
+    asm("v_fma_f32 %1, %3, %5, %0\n\tv_fma_f32 %2, -%3, %5, %4\n\tv_max_f32 %0, %1, %2"
+        : "+{v60}"(V), "=&v"(t1), "=&v"(t2) : "v"(m), "v"(vp), "v"(sg));
+}
 
-// int32 stages (TgFmt::INT): the same three forms on integer patterns
-// two-op form: a = V + m, b = V - m, V' = max(a, b of the partner) -- the partner has the same label and
-// tag outside M_B32's phase-0 rows, so its b is this lane's exchanged candidate
+// int32 stages (TgFmt::INT): the same forms on integer patterns
 template <int Q>
 __device__ __forceinline__ void tg_stage_dpp_i2(float& V, float m)
 {
@@ -206,29 +187,6 @@ __device__ __forceinline__ void tg_stage_dpp_i2(float& V, float m)
     else if constexpr (Q == 2) VD_TG_DPPI2("row_half_mirror");
     else VD_TG_DPPI2("row_ror:8");
 #undef VD_TG_DPPI2
-}
-// three-op form (tools, ABL 1<<24)
-template <int Q>
-__device__ __forceinline__ void tg_stage_dpp_i(float& V, float m)
-{
-    float t1, t2;
-#define VD_TG_DPPI(CTRL)                                                                                  \
-    asm("v_add_u32 %1, %0, %3\n\ts_nop 0\n\tv_sub_u32_dpp %2, %0, %3 " CTRL " row_mask:0xf bank_mask:0xf\n\t" \
-        "v_max_i32 %0, %1, %2"                                                                           \
-        : "+{v60}"(V), "=&v"(t1), "=&v"(t2) : "v"(m))
-    if constexpr (Q == 0) VD_TG_DPPI("quad_perm:[1,0,3,2]");
-    else if constexpr (Q == 1) VD_TG_DPPI("quad_perm:[2,3,0,1]");
-    else if constexpr (Q == 2) VD_TG_DPPI("row_half_mirror");
-    else VD_TG_DPPI("row_ror:8");
-#undef VD_TG_DPPI
-}
-// xor-32 swap stage: e = this lane's signed pair, (E-, -E+) in the lower position half, (-E-, E+) in the
-// upper one, so both halves form [a, b] = [V + e.x, V + e.y] and swap as the fp32 stage does
-__device__ __forceinline__ void tg_stage_swap_i(float& V, f2v e)
-{
-    asm("v_add_u32 v62, %0, %1\n\tv_add_u32 v63, %0, %2\n\ts_nop 1\n\tv_permlane32_swap_b32 v62, v63\n\t"
-            "v_max_i32 %0, v62, v63"
-            : "+{v60}"(V) : "v"(e.x), "v"(e.y) : "v62", "v63");
 }
 __device__ __forceinline__ void tg_stage_lds_i(float& V, float m, float vp)
 {
@@ -358,7 +316,8 @@ struct TgIn<SOFT8> {  // 2 stages per word; the 16-bit half g^1 holds s0 (high b
         A = s0 + s1;
         B = s0 - s1;
     }
-    // the two soft values as floats (sign-extending byte converts): the table row is then six exact FMAs, E[3], E[2] = s1 * +-2^S + (s0 * 2^S + tag), E[0], E[1] = s1 * -+2^S + (-s0 * 2^S + tag)
+    // the two soft values as floats (sign-extending byte converts): the table row is then six exact FMAs,
+    // E[3], E[2] = s1 * +-2^S + (s0 * 2^S + tag), E[0], E[1] = s1 * -+2^S + (-s0 * 2^S + tag)
     static constexpr bool S01 = true;
     static __device__ __forceinline__ void s01(raw_t w, float& s0, float& s1)
     {
@@ -397,8 +356,7 @@ struct TgIn<FP32> {  // 2 floats per stage, clamped to [-8,7]; BM = (int)(+-x0 +
     template <int R>
     static __device__ __forceinline__ raw_t load(__amdgpu_buffer_rsrc_t rs, uint32_t vo)
     {
-        typedef float f2 __attribute__((ext_vector_type(2)));
-        const f2 v = __builtin_bit_cast(f2, __builtin_amdgcn_raw_buffer_load_b64(rs, vo + R * RB, 0, 0));
+        const f2v v = __builtin_bit_cast(f2v, __builtin_amdgcn_raw_buffer_load_b64(rs, vo + R * RB, 0, 0));
         return make_float2(v.x, v.y);
     }
     static __device__ __forceinline__ void ab(raw_t v, int, int& A, int& B, float)
@@ -497,22 +455,22 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t tg_rsrc(const void* in, uint64
 // decoded whole, one per wave, and each remaining chunk by one workgroup as kWaves pieces, so every
 // SIMD gets 6 whole chunks and one piece.  Piece 0 starts at the chunk start (exact).  Piece q > 0
 // starts kSplitWarm blocks before its first word's emit block from equal metrics; at that boundary
-// block it stores its renormalised metric vector (its start vector), and piece q-1 stores its own
+// block it records its renormalised metric vector (its start vector), and piece q-1 records its own
 // vector at the same block (its end vector).  Equal vectors mean every later decision of piece q equals
 // the exact decode's (the recursion and the tie rules depend only on metric differences; V at a block
 // start is VBASE + (metric - metric of position 0) * 2^S with cleared fields), so piece q is verified
-// when piece q-1 is and the two vectors agree.  After each pass the workgroup synchronises (s_barrier)
-// and every wave evaluates the same checks.  Each unverified piece then re-decodes its words from its
-// boundary block, starting from the latest end vector of its left neighbour, and the checks repeat.  The
-// first unverified piece always restarts from an exact vector, so every pass verifies at least one more
-// piece: at most kWaves - 1 re-decode passes, no timeouts, no flags.  Writes of a later pass follow the
-// barrier, so the last (verified) decode of every word is the one that stays.  Block boundaries are
-// multiples of 3 (the group length, 96 stages = 16 trellis periods) so every run uses the same position
-// <-> state map there.  The pieces of a chunk are the waves of one workgroup (one CU), so all vectors are
-// exchanged through workgroup-visible global memory; nothing leaves the XCD's L2.
+// when piece q-1 is and the two vectors agree.  After each pass every piece that ran publishes its two
+// vectors in its own (now dead) table LDS, the workgroup synchronises (s_barrier) and every wave
+// evaluates the same checks.  Each unverified piece takes its left neighbour's end vector into a register,
+// a second barrier lets everyone finish reading, and the unverified pieces re-decode their words from
+// their boundary blocks.  The first unverified piece always restarts from an exact vector, so every pass
+// verifies at least one more piece: at most kWaves - 1 re-decode passes, no timeouts, no flags.  Writes of
+// a later pass follow the barriers, so the last (verified) decode of every word is the one that stays.
+// Block boundaries are multiples of 3 (the group length, 96 stages = 16 trellis periods) so every run
+// uses the same position <-> state map there.  The vectors never leave the workgroup's LDS, so
+// concurrent split launches share no storage.
 constexpr int kSplitWarm = 6;                // warm-up blocks of a speculative piece (multiple of 3)
 constexpr int kSplitMinWords = 64;           // chunks of fewer 32-bit words are not split (host side)
-constexpr int kSplitVecs = 3 * kWaves;       // per split chunk: start[q], end[parity 0][q], end[parity 1][q]
 struct SplitGeo {
     uint32_t s0, words, E;
     int Xspec, Xcmp;
@@ -537,50 +495,34 @@ __device__ __forceinline__ SplitGeo split_geo(uint32_t Sc, int q)
     g.Xcmp = q == kWaves - 1 ? -1 : (int)(kn + 1 - g.s0);
     return g;
 }
-__device__ __forceinline__ int split_start_vec(int q) { return q; }
-__device__ __forceinline__ int split_end_vec(int q, uint32_t par) { return kWaves * (1 + (int)par) + q; }
-// both vectors equal in every lane (wave-uniform)
-__device__ __forceinline__ bool split_vec_eq(const float* vecs, int a, int b, int lane)
-{
-    const uint32_t x = __builtin_bit_cast(uint32_t, vecs[a * 64 + lane]);
-    const uint32_t y = __builtin_bit_cast(uint32_t, vecs[b * 64 + lane]);
-    return __ballot(x != y) == 0;
-}
 
-// ================================================================ tagged kernel: one chunk per wave
+// ================================================================ the kernel: one chunk per wave
 template <int CH, int CORE, int OB, int ABL = 0>
-__global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu((ABL & kAbl7w) ? 7 : 8))) void vd_decode_tg(const void* __restrict__ in_all, void* __restrict__ out_all, Geom geo)
+__global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(8))) void vd_decode_tg(const void* __restrict__ in_all, void* __restrict__ out_all, Geom geo)
 {
     using IN = TgIn<CH>;
-    using FMT = TgFmt<CH, ABL>;
+    using FMT = TgFmt<CH>;
     constexpr bool INT = FMT::INT;
-    static_assert(!INT || CORE == B32 || FMT::I16, "int32 patterns: SOFT16 on the int32 core only");
-    // xor-32 (Q=5) exchange: the partner's metric through the LDS crossbar (ds_bpermute, then three
-    // plain VALU ops) instead of v_permlane32_swap (pk_fma, swap, max).  ABL 8192 (tools): the swap.
-    constexpr bool BP5 = !(ABL & 8192);
-    // M_B32 with the LDS exchange (S32): its phase-0 tie rule differs between the position halves (upper
+    static_assert(!INT || CORE == B32, "int32 patterns: SOFT16 on the int32 core only");
+    // M_B32 on the fp32 patterns (S32): its phase-0 tie rule differs between the position halves (upper
     // half: own wins, tag +2^j).  Instead of rows holding both tag signs, the upper lanes read the entry of
     // the complementary label in the ordinary row (tag -2^j) and negate it: BM[3-L] = -BM[L], so
     // -(BM[3-L]*2^S - 2^j) = BM[L]*2^S + 2^j.  The stage then forms V + s*e and V_partner - s*e with
-    // s = -1 in the upper half (v_fma, as cheap as v_add): the same values as before, and the M_B32 table
-    // becomes the M_B16 one (no pair rows: fewer LDS reads and writes).
-    constexpr bool S32 = CORE == B32 && BP5 && !INT;  // INT keeps the pair rows: the lane reads its half
-    // DPP stages as v_sub, v_add, v_max_f32_dpp (the partner's V - m through the DPP operand) instead of
-    // v_add, v_sub_f32_dpp, v_max: the same decisions; 1 % faster on M_B32 and 0.5 % on M_B16 under bench
-    // conditions (profiles/r02/benchab_*.log).  ABL 262144 (tools): the three-op form.
-    constexpr bool DPP2 = (ABL & 262144) == 0;
-    using TT = TgTab<S32 ? B16 : CORE>;
+    // s = -1 in the upper half (v_fma, as cheap as v_add), and the M_B32 table is the M_B16 one.  SOFT16
+    // (INT) keeps the pair rows: each lane reads its own tag sign's half.
+    constexpr bool S32 = CORE == B32 && !INT;
+    using TT = TgTab<INT>;
+    using LL = TgLds<INT, (ABL & kAblNoGuardSpace) ? 0 : kGuardWords>;
     constexpr int J = FMT::J, S = FMT::S;
-    constexpr int TBS = (ABL & kAbl7w) ? 13 : TgRing<CORE>::TBS;
-    __shared__ __attribute__((aligned(16))) char tab_all[kWaves][TT::BYTES];
-    __shared__ __attribute__((aligned(256))) uint32_t ring_all[kWaves][(TBS + 1) * 64];  // bit 31-s = stage s
+    __shared__ __attribute__((aligned(16))) uint32_t lds[kWaves * LL::WAVE];
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int pos = tg_pos(lane);
-    char* tabb = tab_all[wv];
-    uint32_t* ring = ring_all[wv];
+    uint32_t* const wlds = lds + wv * LL::WAVE;
+    char* const tabb = (char*)(wlds + LL::TAB_OFF);
+    uint32_t* const ring = wlds + LL::RING_OFF;
     // This wave's work: chunk blockIdx.x * kWaves + wv, or, in a split launch (Geom::nwhole), piece wv of
-    // chunk nwhole + (blockIdx.x - nwhole / kWaves) -- see "split chunks" at the end of the file.
+    // chunk nwhole + (blockIdx.x - nwhole / kWaves) -- see "split chunks" above.
     // A batched launch (Geom::nbatch > 1) decodes chunk c of batch b at launch chunk b * nchunks + c.
     const bool split = geo.nwhole != 0 && blockIdx.x >= geo.nwhole / kWaves;
     const uint32_t gchunk = split ? geo.nwhole + (blockIdx.x - geo.nwhole / kWaves) : blockIdx.x * kWaves + wv;
@@ -591,14 +533,13 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu((AB
     const int piece = split ? wv : -1;
     const ChunkRange cr = chunk_range(geo, chunk);
     if (cr.words == 0) return;  // never in a split workgroup: split chunks have >= kSplitMinWords words
-    const uint64_t t_clk0 = (ABL & 32) ? __builtin_amdgcn_s_memtime() : 0;
-    const uint64_t t_rt0 = (ABL & 32) ? __builtin_amdgcn_s_memrealtime() : 0;
+    // guard words (Geom::check): a uniform branch, nothing when off
+    if (geo.check && lane < 3 * kGuardWords && LL::WAVE != LL::TAB + LL::RING) wlds[LL::guard(lane)] = kGuardPattern;
+    const uint64_t t_clk0 = (ABL & kAblClock) ? __builtin_amdgcn_s_memtime() : 0;
+    const uint64_t t_rt0 = (ABL & kAblClock) ? __builtin_amdgcn_s_memrealtime() : 0;
     const uint32_t Sc = OB == 32 ? cr.words : (cr.words + 1) / 2;  // 32-bit words traced back (chunk)
-    float* const svec = split ? geo.spec + (size_t)(chunk - geo.nwhole) * kSplitVecs * 64 : nullptr;
 
-    // per-lane LDS byte addresses of this position's table entries (row offsets are compile-time)
-    // per-lane LDS byte offset of this position's entry in a phase-K row (row offsets are compile-time);
-    // [sx, -sx] route the swap stages' candidates (see tg_stage_swap and the file header)
+    // per-lane LDS byte offset of this position's entry in a phase-K row (row offsets are compile-time)
     const bool upper5 = (pos >> 5) & 1;
     int aK[6];
     sfor<6>([&](auto KK) {
@@ -607,14 +548,8 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu((AB
     });
     if constexpr (S32) aK[0] = upper5 ? 24 - aK[0] : aK[0];  // upper half: the complementary label 3 - L
     const float sg0 = upper5 ? -1.0f : 1.0f;                  // S32: sign of the phase-0 entry
-    // INT phase-0 swap stage: this lane's signed pair, read as two dwords of the (E-, E+) pair row:
-    // (E-[L], -E+[L]) = (E-[L], E-[3-L]) in the lower position half, (-E-[L], E+[L]) = (E+[3-L], E+[L]) in
-    // the upper one (BM[3-L] = -BM[L])
-    const int L0 = own_label(pos, 0);
-    const int aPx = upper5 ? 8 * (3 - L0) + 4 : 8 * L0, aPy = upper5 ? 8 * L0 + 4 : 8 * (3 - L0);
-    const int aU0 = aK[0] + (upper5 ? 4 : 0);  // M_B32 phase-0 pair row: this lane's (E-, E+) half
-    const int pa5 = 4 * (lane ^ 32);  // ds_bpermute address of the xor-32 partner (tools variant)
-    const f2v sxp = upper5 ? (f2v){-1.0f, 1.0f} : (f2v){1.0f, -1.0f};  // the xor-32 swap's [sx, -sx]
+    const int aU0 = aK[0] + (upper5 ? 4 : 0);  // INT phase-0 pair row: this lane's (E-, E+) half
+    const int pa5 = 4 * (lane ^ 32);           // ds_bpermute address of the xor-32 partner
     // table-build roles: every lane writes row `lane` (stages 0..63 of the group), lanes 0..31 also
     // row 64 + lane; J divides 32, so the tag position (row % J) is lane % J for both.  (Writing rows
     // 0..59 of the next group a block ahead, when they are dead, measured no faster:
@@ -625,26 +560,24 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu((AB
     const int rowb1 = TT::row(lane), rowb2 = TT::row(64 + (int)li);
 
     // V lives in [2^23, 2^24), where the fp32 ulp is 1 and the low mantissa bits ARE the low integer
-    // bits: V = 1.5*2^23 + metric*2^S + 2^(S-1) + h.  The 2^(S-1) offset keeps the history field
+    // bits: V = 1.25*2^23 + metric*2^S + 2^(S-1) + h.  The 2^(S-1) offset keeps the history field
     // 2^(S-1) + h in (0, 2^S), so read-out and clearing are bit operations on the pattern.
     // INT: V = metric*2^S + 2^(S-1) + h as an int32, no base needed.
-    // RN16 (ABL bit 27, tools): renormalise every 16 stages around 1.5*2^23 (before r02's last commits)
-    constexpr bool RN16 = (ABL & kAblRn16) != 0;
-    constexpr uint32_t VBASE = (INT ? 0u : RN16 ? 0x4B400000u : 0x4B200000u) + (1u << (S - 1));  // 1.25*2^23 + 2^(S-1)
+    constexpr uint32_t VBASE = (INT ? 0u : 0x4B200000u) + (1u << (S - 1));  // 1.25*2^23 + 2^(S-1)
     const uint32_t fnm = ~((1u << S) - 1u), fhf = 1u << (S - 1);  // field clear: (p & fnm) | fhf
-    Fair fair;  // fairness controller (vd_kernels.h; ABL & 256 disables)
+    Fair fair;  // fairness controller (vd_kernels.h)
     // In a batched launch only the last batch's waves run the controller: earlier batches' waves are
     // followed by more work on their SIMD, so evening out progress buys nothing there and costs issue
-    // (1.6 % per batch, profiles/r02/benchab_fair2.log).  ABL bit 29 (tools): every batch.
-    if constexpr (!(ABL & 256))
-        fair.begin(!(ABL & kAblFairAll) && batch + 1 < geo.nbatch ? nullptr : geo.fair, lane);
+    // (1.6 % per batch, profiles/r02/benchab_fair2.log).
+    if constexpr (!(ABL & kAblNoFair)) fair.begin(batch + 1 < geo.nbatch ? nullptr : geo.fair, lane);
     const uint64_t availB = IN::bytes(geo.availStages);
     const uint32_t vo1 = IN::voff(lane), vo2 = IN::voff((int)li);
-    // split workgroups (uniform bookkeeping): bit q of `verified` = piece q checked exact, bit q of
-    // `endpar` = which end-vector buffer holds piece q's latest end vector
-    uint32_t verified = 1u, endpar = 0u;
+    // split workgroups (uniform bookkeeping): bit q of `verified` = piece q checked exact.  vS / vE: this
+    // piece's start / end vector; vIn: the vector a re-decode starts from (left neighbour's end vector).
+    uint32_t verified = 1u;
+    float vS = 0.0f, vE = 0.0f, vIn = 0.0f;
     for (int pass = 0;; pass++) {
-    const bool runs = piece < 0 || !((verified >> piece) & 1u) || pass == 0;
+    const bool runs = piece < 0 || pass == 0 || !((verified >> piece) & 1u);
     if (runs) {
     // the words of this run: [s0, s0 + Sw) of the chunk, written from word s0 + E on; Xspec / Xcmp: the
     // group-start blocks of the piece's left / right boundary (-1: none)
@@ -662,16 +595,12 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu((AB
     const uint64_t wOut = cr.startWord + s0;  // O_B32: output word of local word 0
     const uint64_t start = (uint64_t)cr.startWord * OB + 32ull * s0;  // first stage of the run
     const uint32_t nblk = Sw + 2;
-    float V = __builtin_bit_cast(float, VBASE);
     // a re-decode starts at the piece's boundary block from its left neighbour's latest end vector
+    float V = pass == 0 ? __builtin_bit_cast(float, VBASE) : vIn;
+    if (pass > 0) vS = V;
     const uint32_t j0 = pass == 0 ? 0u : (uint32_t)Xspec;
-    if (pass > 0) {  // piece >= 1 here (piece 0 is exact and never re-decodes)
-        const int pl = piece > 0 ? piece - 1 : 0;
-        V = svec[split_end_vec(pl, (endpar >> pl) & 1u) * 64 + lane];
-        svec[split_start_vec(piece) * 64 + lane] = V;
-    }
     uint32_t kb = 0;
-    uint32_t tbn = pass == 0 ? TBS - 3 * (blockIdx.x & 3) : TBS;
+    uint32_t tbn = pass == 0 ? kTbs - 3 * (blockIdx.x & 3) : kTbs;
     __amdgpu_buffer_rsrc_t rs = tg_rsrc<CH>(in, start + 32ull * j0, availB);
     typename IN::raw_t rA = IN::template load<0>(rs, vo1);  // stage `lane` of the group
     typename IN::raw_t rB = IN::template load<2>(rs, vo2);  // stage 64 + li
@@ -682,20 +611,16 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu((AB
     // program order -- left alone the compiler merges neighbours into ds_read2_b64 (8 cycles).
     constexpr int TGD = 4;  // 6 or 8 measured the same (profiles/r02/ablate_prefetch.log)
     typedef __attribute__((address_space(3))) const volatile f2v* lptr;
+    typedef __attribute__((address_space(3))) const volatile float* lptr1;
     const __attribute__((address_space(3))) char* tl = (const __attribute__((address_space(3))) char*)tabb;
-    f2v vp[96];  // entry pair read for stage r (even period of a pair, or every M_B32 phase-0 stage)
+    f2v vp[96];  // entry pair read for stage r (even period of a pair, or every INT phase-0 stage)
     auto issue = [&](auto Rc) {
         constexpr int r = decltype(Rc)::value;  // stage within the group (the group starts at phase 0)
         constexpr int K = r % 6;
-        if constexpr (ABL & 2) {
-        } else if constexpr (BP5 && TT::pairrow(K)) {
-            // xor-32 stage through the LDS crossbar on M_B32's phase-0 rows: this lane's tag sign only
-            typedef __attribute__((address_space(3))) const volatile float* lptr1;
+        if constexpr (ABL & kAblNoTabReads) {
+        } else if constexpr (TT::pairrow(K)) {  // INT phase 0: this lane's tag sign only
             vp[r] = (f2v){*(lptr1)(tl + aU0 + TT::row(r)), 0.0f};
-        } else if constexpr (INT && TT::pairrow(K)) {
-            typedef __attribute__((address_space(3))) const volatile float* lptr1;
-            vp[r] = (f2v){*(lptr1)(tl + aPx + TT::row(r)), *(lptr1)(tl + aPy + TT::row(r))};
-        } else if constexpr (TT::pairrow(K) || (r / 6) % 2 == 0) {
+        } else if constexpr ((r / 6) % 2 == 0) {
             vp[r] = *(lptr)(tl + aK[K] + TT::row(r));
         }
     };
@@ -708,56 +633,31 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu((AB
             constexpr int K = (PH + i) % 6;
             constexpr int Q = (K + 5) % 6;
             constexpr int r = 32 * BB + i;  // stage within the group
-            // ABL (tools only): 2 = no table reads, 128 = every stage a DPP stage, 4 = no field read-out
             constexpr bool ODD = (r / 6) % 2 == 1;
             constexpr int RP = TT::pairrow(K) ? r : (ODD ? r - 6 : r);  // where this stage's pair was read
-            // The position bit on lane xor 16 (Q=4) fetches the partner's metric through the LDS crossbar
-            // (ds_swizzle); Q=5 (xor 32) through ds_bpermute or with the v_permlane32_swap candidate swap
-            // (BP5 above): a VALU lane swap costs ~2 DPP ops of issue, the LDS exchange one round trip
-            // queued behind the table reads.
-            constexpr bool IS16 = Q == 4, IS32 = Q == 5;
-            constexpr int DCTRL = Q <= 3 ? Q : 3;  // lane xor 1, 2, 7, 8 -> DPP control
-            constexpr bool LSW = (IS32 && BP5) || IS16;
-            if constexpr (INT) {  // int32 patterns (SOFT16): DPP, xor-32 bpermute (ABL 8192: swap), xor-16 swizzle
-                // DPP stages in the two-op form (sub, add, max with the partner's b through DPP): 5 %
-                // faster than add, sub_dpp, max on int32 (tools/vd_ablate; ABL 1<<24: the three-op form)
-                if constexpr (Q <= 3 && !(ABL & (1 << 24))) tg_stage_dpp_i2<Q>(V, ODD ? vp[RP].y : vp[RP].x);
-                else if constexpr (Q <= 3) tg_stage_dpp_i<Q>(V, ODD ? vp[RP].y : vp[RP].x);
-                else if constexpr (Q == 5 && BP5)
-                    tg_stage_lds_i(V, TT::pairrow(K) || !ODD ? vp[RP].x : vp[RP].y, tg_partner(V, pa5));
-                else if constexpr (Q == 5) tg_stage_swap_i(V, vp[RP]);
-                else {
-                    const float pv = __builtin_bit_cast(float, __builtin_amdgcn_ds_swizzle(__builtin_bit_cast(int, V), 0x401F));
-                    tg_stage_lds_i(V, ODD ? vp[RP].y : vp[RP].x, pv);
-                }
-            } else if constexpr (((!IS16 && !IS32) || (ABL & 128)) && DPP2 && !TT::pairrow(K)) {
-                const float m = (ABL & 2) ? (float)aK[K] : (ODD ? vp[RP].y : vp[RP].x);
-                tg_stage_dpp2<DCTRL>(V, m);
-            } else if constexpr ((!IS16 && !IS32) || (ABL & 128)) {
-                const float m = (ABL & 2) ? (float)aK[K] : (ODD ? vp[RP].y : vp[RP].x);
-                tg_stage_dpp<DCTRL>(V, m);
-            } else if constexpr (LSW && S32 && IS32) {
-                const float pv = tg_partner(V, pa5);
-                const f2v e = (ABL & 2) ? (f2v){(float)aK[K], 1.0f} : vp[RP];
-                tg_stage_lds_sg<ODD ? 1 : 0>(V, e, pv, sg0);
-            } else if constexpr (LSW) {
-                const float pv = IS16 ? __builtin_bit_cast(float, __builtin_amdgcn_ds_swizzle(__builtin_bit_cast(int, V), 0x401F))
-                                      : tg_partner(V, pa5);
-                const f2v e = (ABL & 2) ? (f2v){(float)aK[K], 1.0f} : vp[RP];
-                tg_stage_lds<TT::pairrow(K) ? (BP5 ? 0 : 2) : (ODD ? 1 : 0)>(V, e, pv, upper5);
+            const f2v e = (ABL & kAblNoTabReads) ? (f2v){(float)aK[K], 1.0f} : vp[RP];
+            const float m = TT::pairrow(K) || !ODD ? e.x : e.y;
+            // Q = 0..3: DPP stage (lane xor 1, 2, 7, 8); Q = 4: xor 16 through ds_swizzle; Q = 5: xor 32
+            // through ds_bpermute
+            if constexpr (INT) {
+                if constexpr (Q <= 3) tg_stage_dpp_i2<Q>(V, m);
+                else if constexpr (Q == 4) tg_stage_lds_i(V, m, tg_swz16(V));
+                else tg_stage_lds_i(V, m, tg_partner(V, pa5));
             } else {
-                const f2v e = (ABL & 2) ? (f2v){(float)aK[K], 1.0f} : vp[RP];
-                tg_stage_swap<TT::pairrow(K) ? 2 : (ODD ? 1 : 0)>(V, e, sxp);
+                if constexpr (Q <= 3) tg_stage_dpp2<Q>(V, m);
+                else if constexpr (Q == 4) tg_stage_lds(V, m, tg_swz16(V));
+                else if constexpr (S32) tg_stage_lds_sg(V, m, tg_partner(V, pa5), sg0);
+                else tg_stage_lds(V, m, tg_partner(V, pa5));
             }
             if constexpr (r + TGD < 96) issue(std::integral_constant<int, r + TGD>{});
-            if constexpr (i % J == J - 1 && !(ABL & 4)) {
+            if constexpr (i % J == J - 1 && !(ABL & kAblNoReadout)) {
                 // field read-out: bits 1..J of the pattern, (2^(S-1) + h) >> 1 = (h + 2^J - 1) / 2, go straight
                 // into byte / half g of the block's ring word (SDWA dst_sel: one op for shift and merge), then
                 // the field is cleared to 2^(S-1).  At the end of every block (32 stages) the decision-neutral
                 // renormalisation by the metric of position 0 follows: readfirstlane (1 wait state after the
                 // clear), the offset on the scalar unit, one vector subtract.  s_sub_u32 writes SCC: the
                 // statements with VD_TG_RN declare it clobbered (without that, a compiler that keeps a branch
-                // condition in SCC across them decodes wrong words: the loop-wrapped study kernel did).
+                // condition in SCC across them decodes wrong words: profiles/r02/scc_clobber_check.log).
                 constexpr int g = (i % 32) / J;
                 uint32_t sr;
 #define VD_TG_RO(SEL, UNUSED) "v_lshrrev_b32_sdwa %[w], 1, %[V] dst_sel:" SEL " dst_unused:" UNUSED             \
@@ -766,16 +666,12 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu((AB
 #define VD_TG_IN [fnm] "v"(fnm), [fhf] "v"(fhf), [vb] "n"(VBASE)
                 if constexpr (J == 8 && g == 0)
                     asm(VD_TG_RO("BYTE_0", "UNUSED_PAD") : [V] "+{v60}"(V), [w] "=&v"(word) : VD_TG_IN);
-                else if constexpr (J == 8 && g == 1 && RN16)
-                    asm(VD_TG_RO("BYTE_1", "UNUSED_PRESERVE") VD_TG_RN : [V] "+{v60}"(V), [w] "+v"(word), [sr] "=&s"(sr) : VD_TG_IN : "scc");
                 else if constexpr (J == 8 && g == 1)
                     asm(VD_TG_RO("BYTE_1", "UNUSED_PRESERVE") : [V] "+{v60}"(V), [w] "+v"(word) : VD_TG_IN);
                 else if constexpr (J == 8 && g == 2)
                     asm(VD_TG_RO("BYTE_2", "UNUSED_PRESERVE") : [V] "+{v60}"(V), [w] "+v"(word) : VD_TG_IN);
                 else if constexpr (J == 8)
                     asm(VD_TG_RO("BYTE_3", "UNUSED_PRESERVE") VD_TG_RN : [V] "+{v60}"(V), [w] "+v"(word), [sr] "=&s"(sr) : VD_TG_IN : "scc");
-                else if constexpr (g == 0 && RN16)
-                    asm(VD_TG_RO("WORD_0", "UNUSED_PAD") VD_TG_RN : [V] "+{v60}"(V), [w] "=&v"(word), [sr] "=&s"(sr) : VD_TG_IN : "scc");
                 else if constexpr (g == 0)
                     asm(VD_TG_RO("WORD_0", "UNUSED_PAD") : [V] "+{v60}"(V), [w] "=&v"(word) : VD_TG_IN);
                 else
@@ -789,16 +685,14 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu((AB
         // ends at p at the end of history field g of this block, stage 8g+j (16g+j) at bit j of it;
         // the bits mark the tie-winning candidate, i.e. the take-bit except where the own one wins (F16)
         if constexpr (CORE == F16) word = ~word;
-        if constexpr (ABL & 64) ((uint32_t*)out + (1u << 20))[j * 64 + pos] = word;  // tools: ring words
         wave_sync();
         if (j >= 1) ring[(j - 1 - kb) * 64 + pos] = word;
         if (j >= 2 && (j - 1 - kb == tbn || j == nblk - 1)) {
             wave_sync();
             const uint32_t nw = j - 1 - kb;
-            if (!(ABL & 1) && (uint32_t)lane < nw && kb + lane >= E) {
+            if (!(ABL & kAblNoTraceback) && (uint32_t)lane < nw && kb + lane >= E) {
                 const uint32_t k = kb + (uint32_t)lane;
-                const uint32_t Q0 = (uint32_t)(wv * (TBS + 1) * 256 + (lane + 1) * 256);
-                uint32_t w = traceback_word_tg<J, CORE == B32>((const char*)ring_all, Q0, k);
+                uint32_t w = traceback_word_tg<J, CORE == B32>((const char*)ring, (uint32_t)(lane + 1) * 256u, k);
                 if constexpr (OB == 32) {
                     ((uint32_t*)out)[wOut + k] = w;
                 } else {
@@ -811,23 +705,22 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu((AB
             wave_sync();
             ring[pos] = word;  // block j becomes slot 0 of the next batch
             kb = j - 1;
-            tbn = TBS;
+            tbn = kTbs;
         }
         return j + 1 < nblk;
     };
-    // one 96-stage group's table row from the stage's (A, B) = (BM[3], BM[2])
-    // table row of stage phase K: E[L] = BM[L]*2^S + tag at entries 0, 2, 4, 6 (the odd dwords are the
-    // other period's); M_B32 phase-0 rows: the pairs (E-[L], E+[L]) of both tag signs
+    // table row of stage phase K from the stage's (A, B) = (BM[3], BM[2]): E[L] = BM[L]*2^S + tag at
+    // entries 0, 2, 4, 6 (the odd dwords are the other period's); INT phase-0 rows: the pairs (E-[L], E+[L])
     auto put_row = [&](int rb, auto A, auto B, int K) {  // A, B: ints, or floats (IN::FAB)
-        if constexpr (INT) {  // int32 entries, the fp32 layout (phase-0 rows: the pairs (E-[L], E+[L]))
+        if constexpr (INT) {
             uint32_t* e = (uint32_t*)(tabb + rb);
-            // the tag of the row's own class: +2^j on the F16 core (own wins ties), -2^j elsewhere
+            // the tag of the row's own class: -2^j (the int32 core: exchanged wins ties)
             const int a = A * (1 << S), b = B * (1 << S), tag = -(int)tg0;
             e[0] = (uint32_t)(-a - tag);
             e[2] = (uint32_t)(-b - tag);
             e[4] = (uint32_t)(b - tag);
             e[6] = (uint32_t)(a - tag);
-            if (TT::pairrow(0) && K == 0) {
+            if (K == 0) {
                 e[1] = (uint32_t)(-a + tag);
                 e[3] = (uint32_t)(-b + tag);
                 e[5] = (uint32_t)(b + tag);
@@ -840,7 +733,7 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu((AB
         float* e = (float*)(tabb + rb);
         const float E0 = __builtin_fmaf(af, -SC, tg0), E1 = __builtin_fmaf(bf, -SC, tg0);
         const float E2 = __builtin_fmaf(bf, SC, tg0), E3 = __builtin_fmaf(af, SC, tg0);
-        if constexpr (ABL & 512) {  // tools only: compute the row, do not store it
+        if constexpr (ABL & kAblNoTabWrites) {  // tools only: compute the row, do not store it
             asm volatile("" ::"v"(E0), "v"(E1), "v"(E2), "v"(E3));
             return;
         }
@@ -848,18 +741,10 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu((AB
         e[2] = E1;
         e[4] = E2;
         e[6] = E3;
-        if constexpr (TT::pairrow(0)) {  // M_B32 with the lane swap: phase-0 rows hold both tag signs
-            if (K == 0) {
-                e[1] = __builtin_fmaf(af, -SC, tagv);
-                e[3] = __builtin_fmaf(bf, -SC, tagv);
-                e[5] = __builtin_fmaf(bf, SC, tagv);
-                e[7] = __builtin_fmaf(af, SC, tagv);
-            }
-        }
     };
     // S01: rows from the two soft values (six FMAs) instead of (A, B) = (s0 + s1, s0 - s1) (two integer
-    // ops, two converts, four FMAs); fp32 cores without pair rows.  ABL bit 30 (tools): the (A, B) form.
-    constexpr bool S01 = HasS01<IN>::value && !INT && !TT::pairrow(0) && !(ABL & kAblNoS01);
+    // ops, two converts, four FMAs); fp32 cores
+    constexpr bool S01 = HasS01<IN>::value && !INT;
     auto put_row_s01 = [&](int rb, float s0, float s1) {
         constexpr float SC = (float)(1 << S);
         const float X = __builtin_fmaf(s0, SC, tg0), Y = __builtin_fmaf(s0, -SC, tg0);
@@ -873,7 +758,7 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu((AB
     for (uint32_t j = j0;; j += 3) {
         // group head: the table from the inputs loaded one group ago, the next group's loads, then the
         // fairness board (its load returns during this group; nothing here waits on it)
-        if constexpr (S01 && !(ABL & 8)) {
+        if constexpr (S01 && !(ABL & kAblNoTabBuild)) {
             float s0, s1;
             IN::s01(rA, s0, s1);
             put_row_s01(rowb1, s0, s1);
@@ -881,7 +766,7 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu((AB
                 IN::s01(rB, s0, s1);
                 put_row_s01(rowb2, s0, s1);
             }
-        } else if constexpr (!(ABL & 8)) {  // ABL 8 (tools only): no table build
+        } else if constexpr (!(ABL & kAblNoTabBuild)) {
             using ab_t = std::conditional_t<IN::FAB, float, int>;
             auto ab = [&](const typename IN::raw_t& raw, int l, ab_t& A, ab_t& B) {
                 if constexpr (IN::FAB) IN::abf(raw, l, A, B, geo.scale);
@@ -895,19 +780,17 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu((AB
                 put_row(rowb2, A, B, r6b);
             }
         }
-        if constexpr (!(ABL & 16)) {
+        if constexpr (!(ABL & kAblNoLoads)) {
             rs = tg_rsrc<CH>(in, start + 32ull * (j + 3), availB);
             rA = IN::template load<0>(rs, vo1);
             rB = IN::template load<2>(rs, vo2);
         }
-        if constexpr (!(ABL & 256)) {
-            // every other group head (6 blocks): 0.7 % faster than every head, every third is 1 % slower
-            // (profiles/r02/benchab_fair.log); ABL 1<<25 (tools): every head
-            constexpr uint32_t FE = (ABL & (1 << 25)) ? 1 : 2;
-            if (FE == 1 || (j / 3) % FE == 0) fair.group<3 * (int)FE>(j, lane);
-        }
-        if (split && pass == 0 && (int)j == Xspec) svec[split_start_vec(piece) * 64 + lane] = V;
-        if (split && (int)j == Xcmp) svec[split_end_vec(piece, (uint32_t)pass & 1u) * 64 + lane] = V;
+        // every other group head (6 blocks): 0.7 % faster than every head, every third is 1 % slower
+        // (profiles/r02/benchab_fair.log)
+        if constexpr (!(ABL & kAblNoFair))
+            if ((j / 3) % 2 == 0) fair.group<6>(j, lane);
+        if (split && pass == 0 && (int)j == Xspec) vS = V;
+        if (split && (int)j == Xcmp) vE = V;
         wave_sync();
         sfor<TGD>([&](auto X) { issue(X); });
         if (!block(std::integral_constant<int, 0>{}, j)) break;
@@ -915,22 +798,37 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu((AB
         if (!block(std::integral_constant<int, 4>{}, j + 2)) break;
         wave_sync();
     }
+    if (split) {  // publish the run's vectors in this wave's table LDS (dead after the run)
+        wave_sync();
+        float* pub = (float*)tabb;
+        pub[lane] = vS;
+        pub[64 + lane] = vE;
+    }
     }  // runs
     if (piece < 0) break;
     // split workgroup: evaluate the boundary checks (every wave the same), then re-decode what failed
-    const uint32_t ran = pass == 0 ? (1u << kWaves) - 1u : ~verified & ((1u << kWaves) - 1u);
-    endpar = (endpar & ~ran) | ((pass & 1) ? ran : 0u);
     __syncthreads();
+    auto vec = [&](int q, int which) {  // piece q's start (0) / end (1) vector, this lane's entry
+        return __builtin_bit_cast(uint32_t, ((const float*)(lds + q * LL::WAVE + LL::TAB_OFF))[64 * which + lane]);
+    };
     for (int q = 1; q < kWaves; q++)
-        if (!((verified >> q) & 1u) && ((verified >> (q - 1)) & 1u) &&
-            split_vec_eq(svec, split_start_vec(q), split_end_vec(q - 1, (endpar >> (q - 1)) & 1u), lane))
+        if (!((verified >> q) & 1u) && ((verified >> (q - 1)) & 1u) && __ballot(vec(q, 0) != vec(q - 1, 1)) == 0)
             verified |= 1u << q;
     if (verified == (1u << kWaves) - 1u) break;
-    if (lane == 0 && !((verified >> piece) & 1u) && geo.stats) atomicAdd(geo.stats, 1u);
-    __syncthreads();  // the next pass overwrites vectors read above
+    if (!((verified >> piece) & 1u)) {
+        vIn = __builtin_bit_cast(float, vec(piece - 1, 1));
+        if (lane == 0 && geo.stats) atomicAdd(geo.stats, 1u);
+    }
+    __syncthreads();  // the next pass overwrites the published vectors read above
     }  // pass
-    if constexpr (!(ABL & 256)) fair.end(lane);
-    if constexpr (ABL & 32) {
+    if constexpr (!(ABL & kAblNoFair)) fair.end(lane);
+    if (geo.check) {  // guard words intact?  count the ones that are not
+        wave_sync();
+        const bool bad = lane < 3 * kGuardWords && wlds[LL::guard(lane)] != kGuardPattern;
+        const uint32_t nbad = (uint32_t)__builtin_popcountll(__ballot(bad));
+        if (lane == 0 && nbad) atomicAdd(geo.check, nbad);
+    }
+    if constexpr (ABL & kAblClock) {
         const uint64_t c1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
         if (lane == 0) {
             uint64_t* d = (uint64_t*)((char*)out + (16u << 20)) + 6 * (blockIdx.x * kWaves + wv);

@@ -5,25 +5,25 @@
 // viterbiBM.cuh, viterbiACS.cuh, viterbiTB.cuh), re-designed for CDNA4 wave64.  Not a translation:
 //
 //  * State layout.  A wave64 lane holds ONE trellis state (the reference: a warp32 lane holds two).
-//    Lane p holds, after stage t, the state rotr6(p, t%6).  Under that rotation the radix-2 butterfly
-//    of every stage pairs lanes p and p^(1<<q), q = (t%6+5)%6, so each stage needs one xor-lane
-//    exchange: DPP quad_perm (q=0,1), DPP row_half_mirror+quad_perm (q=2), DPP row_ror:8 (q=3),
-//    ds_swizzle xor-16 (q=4), ds_bpermute xor-32 (q=5).
+//    Position p holds, after stage t, the state rotr6(p, t%6); under that rotation the radix-2 butterfly
+//    of every stage pairs positions p and p^(1<<q), q = (t%6+5)%6, and a linear position -> lane map
+//    turns four of the six butterfly distances into DPP controls fused into the ACS max (quad_perm,
+//    row_half_mirror, row_ror:8); xor-16 and xor-32 go through ds_swizzle / ds_bpermute.
 //  * Metric cores.  Every core (M_B32, M_B16, M_FP16) runs in exact-integer fp32, one chunk per wave;
-//    the metric type only selects the tie rule; SOFT16 runs on int32 patterns.  This file holds the
-//    shared pieces (geometry, chunk partition, fairness controller); vd_kernel_tg.h holds the decode
-//    kernel.
-//  * Survivors.  No register exchange: each stage's decision ("took the exchanged predecessor") is
-//    the sign bit of a candidate difference, accumulated into one word per lane per 32-stage block
-//    that goes to an LDS ring.  Output words are traced back lane-parallel (TB words at a time) in
-//    POSITION space, where a traceback step is p ^= d << q -- no state arithmetic.
-//  * Branch metrics.  Per 32-stage block, 32 lanes compute the 4 branch metrics of one stage each
-//    into an LDS table; every stage each lane reads the metric of its own transition with one
-//    ds_read_b32 whose base register depends only on (lane, t%6).
+//    the metric type only selects the tie rule; SOFT16 runs on int32 patterns.
+//  * Survivors.  Tagged ACS (vd_kernel_tg.h): each stage's decision rides in the low bits of the path
+//    metric, so the max itself does the register exchange within an 8- or 16-stage history field; one
+//    SDWA shift per field moves the field's bits into the block's ring word in LDS.  Output words are
+//    traced back lane-parallel, one dependent LDS byte/half read per field, in POSITION space.
+//  * Branch metrics.  Per 96-stage group, every lane builds table rows (the four label entries of one
+//    stage) into LDS; every stage each lane reads its own transition's entry (one ds_read_b64 serves
+//    two stages of the same phase).
+// This file holds the shared pieces (geometry, chunk partition, fairness controller); vd_kernel_tg.h
+// holds the decode kernel.
 //
 // Decode semantics (bit-exact with the reference for every valid option): see DESIGN.md and
 // oracle/vd_oracle.c.  Tie rules, in own/exchanged terms: M_B16 -> exchanged wins, M_FP16 -> own
-// wins, M_B32 -> exchanged wins except at t%6==0 where the odd predecessor wins (lanes >= 32 keep own).
+// wins, M_B32 -> exchanged wins except at t%6==0 where the odd predecessor wins (upper positions keep own).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -43,10 +43,12 @@ struct Geom {
     uint32_t* fair;        // per-SIMD progress board (kFairBoardWords, empty at rest) or null
     float scale;           // LLR input (channel ids 8 + base): SoftDecisionPacker scale, else unused
     // split launch (vd_kernel_tg.h "split chunks"): chunks >= nwhole are decoded as kWaves pieces, one
-    // workgroup each; 0 = every chunk whole
+    // workgroup each (their boundary vectors stay in the workgroup's LDS); 0 = every chunk whole
     uint32_t nwhole = 0;
-    float* spec = nullptr;       // [chunk - nwhole][kSplitVecs][64] piece boundary metric vectors
     uint32_t* stats = nullptr;   // count of split pieces re-decoded (or null)
+    // LDS guard check (tests): non-null = write guard words around every wave's table and ring and count
+    // the ones found overwritten at kernel exit into *check
+    uint32_t* check = nullptr;
     // several independent batches of the same size in one launch (never split): batch b decodes
     // in + b * inStride bytes into out + b * outStride bytes; chunk c of the launch = chunk c % nchunks
     // of batch c / nchunks

@@ -18,7 +18,9 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libvitdec.so")
+# VITDEC_LIB (tests only): another build of the same C-ABI, e.g. the deliberately broken scratch build
+# tests/test_gpu_guard.py uses to show the LDS guard check catches a real bug
+LIB_PATH = os.environ.get("VITDEC_LIB") or os.path.join(_HERE, "lib", "libvitdec.so")
 
 # ---- option bitmask (reference src/viterbi/viterbi.h:7-20) ----
 CHANNEL_MASK, METRIC_MASK, DECODE_MASK, COMP_MASK = 0xF, 0xF0, 0xF00, 0xF000
@@ -42,7 +44,8 @@ EXPORTS = ["vd_options_valid", "vd_input_size", "vd_message_len", "vd_output_siz
            "vd_create", "vd_destroy", "vd_run", "vd_run_device", "vd_run_device_batch", "vd_run_batches",
            "vd_simulate_host", "vd_count_errors", "vd_last_error", "vd_device_count", "vd_kernel_name",
            "vd_pack_device", "vd_run_device_llr", "vd_run_llr", "vd_host_alloc", "vd_host_free",
-           "vd_run_stream", "vd_channel_device", "vd_simulate_device", "vd_mt_state_after", "vd_split_redecodes"]
+           "vd_run_stream", "vd_channel_device", "vd_simulate_device", "vd_mt_state_after", "vd_split_redecodes",
+           "vd_set_guard_check", "vd_guard_violations"]
 
 
 class VitdecError(RuntimeError):
@@ -77,6 +80,8 @@ def lib():
     L.vd_simulate_device.argtypes = [i, sz, f, ctypes.c_uint32, ctypes.c_uint32, vp, vp, vp]
     L.vd_mt_state_after.argtypes = [ctypes.c_uint32, ctypes.c_uint64, vp]
     L.vd_split_redecodes.argtypes = [i, ctypes.POINTER(ctypes.c_uint64)]
+    L.vd_set_guard_check.argtypes = [vp, i]
+    L.vd_guard_violations.argtypes = [vp, ctypes.POINTER(ctypes.c_uint64)]
     L.vd_count_errors.argtypes = [i, vp, sz, vp, sz]
     L.vd_count_errors.restype = ctypes.c_longlong
     L.vd_last_error.restype = ctypes.c_char_p
@@ -205,6 +210,16 @@ class ViterbiCUDA:
         _check(lib().vd_run_device_batch(self._h, ctypes.c_void_p(input_ptr), input_stride, ctypes.c_void_p(output_ptr),
                                          output_stride, inputNum, nbatch, ctypes.c_void_p(stream)))
 
+    def set_guard_check(self, enable=True):
+        """LDS guard words around every wave's table and ring, counted at kernel exit when overwritten
+        (vd_set_guard_check; the count restarts at 0)."""
+        _check(lib().vd_set_guard_check(self._h, 1 if enable else 0))
+
+    def guard_violations(self):
+        """guard words found overwritten since set_guard_check(True) (synchronises the device)"""
+        v = ctypes.c_uint64(0)
+        _check(lib().vd_guard_violations(self._h, ctypes.byref(v)))
+        return v.value
 
     def run_stream(self, inputs, inputNum=None, outputs=None):
         """Pipelined decode of independent batches (host copies overlapped with decoding).

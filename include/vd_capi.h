@@ -70,7 +70,9 @@ int vd_run(vd_decoder* dec, const void* input_h, void* output_h, size_t inputNum
 
 /* Asynchronous device-to-device decode on `stream` (a hipStream_t passed as void*, NULL = the
  * null stream).  input_d / output_d are device pointers on the decoder's device, sized as above.
- * No allocation, no synchronisation: safe to capture in a hipGraph. */
+ * No allocation, no synchronisation: safe to capture in a hipGraph.  The stream (for NULL: the calling
+ * thread's current device) must belong to the decoder's device, else VD_ERR_ARG.  Launches on any
+ * number of streams may run concurrently: no launch shares device scratch with another. */
 int vd_run_device(vd_decoder* dec, const void* input_d, void* output_d, size_t inputNum, void* stream);
 
 /* nbatch independent batches of inputNum encoded values each in ONE launch (new; for batched callers):
@@ -150,6 +152,13 @@ long long vd_count_errors(int options, const uint8_t* bits, size_t N, const void
  * decoded words are exact either way).  VD_NO_SPLIT=1 in the environment (read once per process and
  * device) disables splitting. */
 int vd_split_redecodes(int device, uint64_t* count);
+/* LDS guard check (tests): enable != 0 makes every later launch of this decoder write guard words around
+ * each wave's branch-metric table and survivor ring in LDS and count, at kernel exit, the guard words
+ * found overwritten (an out-of-bounds LDS store); the count restarts at 0.  Off by default (one uniform
+ * branch per wave when off).  VD_CHECK=1 in the environment turns it on at vd_create. */
+int vd_set_guard_check(vd_decoder* dec, int enable);
+/* guard words found overwritten since the check was enabled (synchronises the device) */
+int vd_guard_violations(vd_decoder* dec, uint64_t* count);
 const char* vd_last_error(void);
 int vd_device_count(void);
 /* last decode kernel's name and grid, for profilers (static strings) */

@@ -9,7 +9,6 @@
 #include <cstring>
 #include <string>
 #include "../gpu-accelerated-viterbi-decoder_amd/csrc/vd_kernel_tg.h"
-#include "vd_ps_kernel.h"
 
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP error %s at %d\n", hipGetErrorString(e), __LINE__); exit(1); } } while (0)
 
@@ -20,7 +19,6 @@ template <int ABL> void tgb(std::vector<Var>& v, const char* n) { v.push_back({n
 template <int ABL> void tgs(std::vector<Var>& v, const char* n) { v.push_back({n, (KFn)vd::vd_decode_tg<vd::SOFT8, vd::B16, 32, ABL>, 1600}); }
 template <int ABL> void tgf(std::vector<Var>& v, const char* n) { v.push_back({n, (KFn)vd::vd_decode_tg<vd::FP32, vd::F16, 32, ABL>, 1600}); }
 template <int ABL> void tgi(std::vector<Var>& v, const char* n) { v.push_back({n, (KFn)vd::vd_decode_tg<vd::SOFT16, vd::B32, 32, ABL>, 1600}); }
-template <int CH, int CORE, int ABL> void psk(std::vector<Var>& v, const char* n) { v.push_back({n, (KFn)vd::vd_decode_ps<CH, CORE, 32, ABL>, 800}); }
 
 int main(int argc, char** argv)
 {
@@ -45,56 +43,31 @@ int main(int argc, char** argv)
     CK(hipMalloc(&g.fair, vd::kFairBoardWords * 4));
     CK(hipMemset(g.fair, 0xFF, vd::kFairBoardWords * 4));
     std::vector<Var> v;
-    tgb<0>(v, "tg hard/b32 full"); tgb<1>(v, "tg hard/b32 -traceback"); tgb<16>(v, "tg hard/b32 -loads"); tgb<256>(v, "tg hard/b32 -fairness");
-    tgb<2>(v, "tg hard/b32 -tabreads"); tgb<4>(v, "tg hard/b32 -readout"); tgb<8>(v, "tg hard/b32 -tabbuild"); tgb<128>(v, "tg hard/b32 all-dpp"); tgb<512>(v, "tg hard/b32 -tabwrites"); tgs<512>(v, "tg soft8/b16 -tabwrites"); tgs<8>(v, "tg soft8/b16 -tabbuild");
-    tgb<2 | 4 | 8 | 16 | 1>(v, "tg hard/b32 ACS only"); tgb<2 | 4 | 8 | 16 | 1 | 128>(v, "tg hard/b32 ACS only all-dpp");
-    tgs<2 | 4 | 8 | 16 | 1>(v, "tg soft8/b16 ACS only");
-    tgi<0>(v, "tg soft16/b32 full"); tgi<8192>(v, "tg soft16/b32 q5 permlane");
-    tgi<8>(v, "tg soft16/b32 -tabbuild"); tgi<4>(v, "tg soft16/b32 -readout");
-    tgi<1>(v, "tg soft16/b32 -traceback"); tgi<2 | 4 | 8 | 16 | 1>(v, "tg soft16/b32 ACS only");
-    tgi<(1 << 24)>(v, "tg soft16/b32 dpp three-op");
-    psk<vd::HARD, vd::B32, 0>(v, "ps hard/b32 full"); psk<vd::SOFT8, vd::B16, 0>(v, "ps soft8/b16 full");
-    psk<vd::SOFT16, vd::B32, 0>(v, "ps soft16/b32 full"); psk<vd::FP32, vd::F16, 0>(v, "ps fp32/f16 full");
-    psk<vd::SOFT8, vd::B16, 1>(v, "ps soft8/b16 -traceback"); psk<vd::SOFT8, vd::B16, 2>(v, "ps soft8/b16 -tabreads");
-    psk<vd::SOFT8, vd::B16, 4>(v, "ps soft8/b16 -readout"); psk<vd::SOFT8, vd::B16, 8>(v, "ps soft8/b16 -tabbuild");
-    psk<vd::SOFT8, vd::B16, 16>(v, "ps soft8/b16 -loads"); psk<vd::SOFT8, vd::B16, 256>(v, "ps soft8/b16 -fairness");
-    psk<vd::SOFT8, vd::B16, 1 | 2 | 4 | 8 | 16>(v, "ps soft8/b16 ACS only");
-    psk<vd::HARD, vd::B32, 1 | 2 | 4 | 8 | 16>(v, "ps hard/b32 ACS only");
-    // balanced grids (every SIMD the same waves): 6144 chunks; the rate is per 6144-chunk launch
+    // component ablations of the product kernels (vd_kernel_tg.h kAbl*): what each part of the kernel
+    // costs, and the ACS-only instruction-mix ceiling bench.py quotes
+    tgb<0>(v, "tg hard/b32 full"); tgb<vd::kAblNoTraceback>(v, "tg hard/b32 -traceback");
+    tgb<vd::kAblNoLoads>(v, "tg hard/b32 -loads"); tgb<vd::kAblNoFair>(v, "tg hard/b32 -fairness");
+    tgb<vd::kAblNoTabReads>(v, "tg hard/b32 -tabreads"); tgb<vd::kAblNoReadout>(v, "tg hard/b32 -readout");
+    tgb<vd::kAblNoTabBuild>(v, "tg hard/b32 -tabbuild"); tgb<vd::kAblNoTabWrites>(v, "tg hard/b32 -tabwrites");
+    tgb<vd::kAblAcsOnly>(v, "tg hard/b32 ACS only");
+    tgs<0>(v, "tg soft8/b16 full"); tgs<vd::kAblNoTraceback>(v, "tg soft8/b16 -traceback");
+    tgs<vd::kAblNoLoads>(v, "tg soft8/b16 -loads"); tgs<vd::kAblNoFair>(v, "tg soft8/b16 -fairness");
+    tgs<vd::kAblNoTabReads>(v, "tg soft8/b16 -tabreads"); tgs<vd::kAblNoReadout>(v, "tg soft8/b16 -readout");
+    tgs<vd::kAblNoTabBuild>(v, "tg soft8/b16 -tabbuild"); tgs<vd::kAblNoTabWrites>(v, "tg soft8/b16 -tabwrites");
+    tgs<vd::kAblAcsOnly>(v, "tg soft8/b16 ACS only");
+    tgi<0>(v, "tg soft16/b32 full"); tgi<vd::kAblNoTabBuild>(v, "tg soft16/b32 -tabbuild");
+    tgi<vd::kAblNoReadout>(v, "tg soft16/b32 -readout"); tgi<vd::kAblNoTraceback>(v, "tg soft16/b32 -traceback");
+    tgi<vd::kAblNoTabReads>(v, "tg soft16/b32 -tabreads"); tgi<vd::kAblAcsOnly>(v, "tg soft16/b32 ACS only");
+    tgf<0>(v, "tg fp32/f16 full"); tgf<vd::kAblNoTabBuild>(v, "tg fp32/f16 -tabbuild");
+    tgf<vd::kAblNoLoads>(v, "tg fp32/f16 -loads"); tgf<vd::kAblAcsOnly>(v, "tg fp32/f16 ACS only");
+    // balanced grid (every SIMD the same waves): 6144 chunks; the rate is per 6144-chunk launch
     v.push_back({"tg soft8/b16 6144 chunks", (KFn)vd::vd_decode_tg<vd::SOFT8, vd::B16, 32, 0>, 1536});
-    v.push_back({"ps soft8/b16 6144 chunks", (KFn)vd::vd_decode_ps<vd::SOFT8, vd::B16, 32, 0>, 768});
-    tgs<0>(v, "tg soft8/b16 full"); tgs<1>(v, "tg soft8/b16 -traceback"); tgs<2>(v, "tg soft8/b16 -tabreads"); tgs<4>(v, "tg soft8/b16 -readout"); tgf<0>(v, "tg fp32/f16 full");
-    tgb<262144>(v, "tg hard/b32 add+subdpp+max"); tgs<262144>(v, "tg soft8/b16 add+subdpp+max");
-    tgs<8192>(v, "tg soft8/b16 q5 permlane");
-    tgb<vd::kAblRn16>(v, "tg hard/b32 rn16"); tgs<vd::kAblRn16>(v, "tg soft8/b16 rn16"); tgf<vd::kAblRn16>(v, "tg fp32/f16 rn16");
-    tgi<vd::kAblRn16>(v, "tg soft16/b32 rn16");
-    tgs<vd::kAblNoS01>(v, "tg soft8/b16 ab rows"); tgs<vd::kAblNoS01 | 8>(v, "tg soft8/b16 -tabbuild ab");
-    tgs<vd::kAblI16>(v, "tg soft8/b16 i16"); tgf<vd::kAblI16>(v, "tg fp32/f16 i16");
-    tgs<vd::kAblI16 | 2 | 4 | 8 | 16 | 1>(v, "tg soft8/b16 i16 ACS only");
-    v.push_back({"tg soft4/b16 full", (KFn)vd::vd_decode_tg<vd::SOFT4, vd::B16, 32, 0>, 1600});
-    v.push_back({"tg soft4/b16 i16", (KFn)vd::vd_decode_tg<vd::SOFT4, vd::B16, 32, vd::kAblI16>, 1600});
-    v.push_back({"tg soft8/b32 full", (KFn)vd::vd_decode_tg<vd::SOFT8, vd::B32, 32, 0>, 1600});
-    v.push_back({"tg soft8/b32 i16", (KFn)vd::vd_decode_tg<vd::SOFT8, vd::B32, 32, vd::kAblI16>, 1600});
-    tgb<8192>(v, "tg hard/b32 q5 permlane"); tgf<8192>(v, "tg fp32/f16 q5 permlane");
-    tgb<8192 | 1>(v, "tg hard/b32 perm32 -traceback"); tgb<8192 | 2>(v, "tg hard/b32 perm32 -tabreads"); tgb<8192 | 4>(v, "tg hard/b32 perm32 -readout");
-    tgb<8192 | 8>(v, "tg hard/b32 perm32 -tabbuild"); tgb<8192 | 16>(v, "tg hard/b32 perm32 -loads"); tgb<8192 | 256>(v, "tg hard/b32 perm32 -fairness"); tgb<2 | 4 | 8 | 16 | 1 | 8192>(v, "tg hard/b32 ACS only q5 permlane"); tgs<2 | 4 | 8 | 16 | 1 | 8192>(v, "tg soft8/b16 ACS only q5 permlane");
     // variants that must decode exactly like the full kernel: outputs compared word for word below
     auto twin = [&](const char* a, const char* b) {
         int ia = -1, ib = -1;
         for (size_t i = 0; i < v.size(); i++) { if (!strcmp(v[i].name, a)) ia = (int)i; if (!strcmp(v[i].name, b)) ib = (int)i; }
         if (ia >= 0 && ib >= 0) v[ib].ref = ia;
     };
-    twin("tg soft16/b32 full", "tg soft16/b32 dpp three-op"); twin("tg soft16/b32 full", "tg soft16/b32 q5 permlane");
-    twin("tg hard/b32 full", "ps hard/b32 full"); twin("tg soft8/b16 full", "ps soft8/b16 full");
-    twin("tg soft16/b32 full", "ps soft16/b32 full"); twin("tg fp32/f16 full", "ps fp32/f16 full");
-    twin("tg fp32/f16 full", "tg fp32/f16 i16"); twin("tg fp32/f16 full", "tg fp32/f16 rn16");
-    twin("tg soft16/b32 full", "tg soft16/b32 rn16"); twin("tg soft4/b16 full", "tg soft4/b16 i16");
-    twin("tg soft8/b32 full", "tg soft8/b32 i16");
-    for (const char* k : {"add+subdpp+max", "q5 permlane", "i16", "ab rows", "rn16"}) {
-        char a[96], b[96];
-        snprintf(a, sizeof a, "tg hard/b32 full"); snprintf(b, sizeof b, "tg hard/b32 %s", k); twin(a, b);
-        snprintf(a, sizeof a, "tg soft8/b16 full"); snprintf(b, sizeof b, "tg soft8/b16 %s", k); twin(a, b);
-    }
     // optional filter (argv[2]): comma-separated name substrings; a kept variant keeps its exact twin
     if (argc > 2) {
         std::vector<int> keep(v.size(), 0);
@@ -158,9 +131,9 @@ int main(int argc, char** argv)
             printf("exact twin %-30s vs %-22s: %zu of %zu words differ\n", v[i].name, r.name, bad, a.size());
         }
     }
-    // per-wave clock stamps of the full kernel (ABL 32), without and with the priority schedule (64)
+    // per-wave clock stamps of the full kernel (kAblClock)
     if (argc <= 2 && nb == 1)  // not with a filter
-    for (KFn f : {(KFn)vd::vd_decode_tg<vd::HARD, vd::B32, 32, 32>}) {
+    for (KFn f : {(KFn)vd::vd_decode_tg<vd::HARD, vd::B32, 32, vd::kAblClock>}) {
         printf("=== tg full\n");
         for (int r = 0; r < 3; r++) hipLaunchKernelGGL(f, dim3(1600), dim3(256), 0, 0, in, out, g);
         CK(hipDeviceSynchronize());

@@ -65,20 +65,14 @@ int main(int argc, char** argv)
     g.scale = 1.0f;
     CK(hipMalloc(&g.fair, vd::kFairBoardWords * 4));
     CK(hipMemset(g.fair, 0xFF, vd::kFairBoardWords * 4));
-    float* spec; uint32_t* stats;
-    CK(hipMalloc(&spec, 256 * vd::kSplitVecs * 64 * 4));
+    uint32_t* stats;
     CK(hipMalloc(&stats, 4));
     CK(hipMemset(stats, 0, 4));
-    g.nwhole = 6144; g.spec = spec; g.stats = stats;
+    g.nwhole = 6144; g.stats = stats;
     const Variant vs[] = {
         {"product (xor-32 by ds_bpermute)", (KFn)vd::vd_decode_tg<vd::HARD, vd::B32, 32, 0>, (KFn)vd::vd_decode_tg<vd::SOFT8, vd::B16, 32, 0>},
         {"no fairness controller (ABL 256)", (KFn)vd::vd_decode_tg<vd::HARD, vd::B32, 32, 256>, (KFn)vd::vd_decode_tg<vd::SOFT8, vd::B16, 32, 256>},
-        {"renormalisation every 16 stages (ABL 27)", (KFn)vd::vd_decode_tg<vd::HARD, vd::B32, 32, vd::kAblRn16>, (KFn)vd::vd_decode_tg<vd::SOFT8, vd::B16, 32, vd::kAblRn16>},
-        {"SOFT8 table rows from (A, B) (ABL 30)", (KFn)vd::vd_decode_tg<vd::HARD, vd::B32, 32, 0>, (KFn)vd::vd_decode_tg<vd::SOFT8, vd::B16, 32, vd::kAblNoS01>},
-        {"fairness on every batch (ABL 29)", (KFn)vd::vd_decode_tg<vd::HARD, vd::B32, 32, vd::kAblFairAll>, (KFn)vd::vd_decode_tg<vd::SOFT8, vd::B16, 32, vd::kAblFairAll>},
-        {"7 waves per SIMD, 13 ring slots (ABL 7W)", (KFn)vd::vd_decode_tg<vd::HARD, vd::B32, 32, vd::kAbl7w>, (KFn)vd::vd_decode_tg<vd::SOFT8, vd::B16, 32, vd::kAbl7w>},
-        {"8 waves, fairness every batch, renormalisation every 16, (A, B) rows (mid-round state)", (KFn)vd::vd_decode_tg<vd::HARD, vd::B32, 32, vd::kAblFairAll | vd::kAblRn16>, (KFn)vd::vd_decode_tg<vd::SOFT8, vd::B16, 32, vd::kAblFairAll | vd::kAblRn16 | vd::kAblNoS01>},
-        {"DPP stages in the three-op form (add, sub_dpp, max)", (KFn)vd::vd_decode_tg<vd::HARD, vd::B32, 32, 262144>, (KFn)vd::vd_decode_tg<vd::SOFT8, vd::B16, 32, 262144>},
+        {"no LDS guard space (19,968 B per workgroup)", (KFn)vd::vd_decode_tg<vd::HARD, vd::B32, 32, vd::kAblNoGuardSpace>, (KFn)vd::vd_decode_tg<vd::SOFT8, vd::B16, 32, vd::kAblNoGuardSpace>},
     };
     const int nv = sizeof(vs) / sizeof(vs[0]);
     // bench conditions (bench.py): each workload's `steps` batches as one batched launch, every batch its
@@ -95,7 +89,7 @@ int main(int argc, char** argv)
         CK(hipMemcpy((char*)bS + k * strS, inS, hs.size() * 4, hipMemcpyDeviceToDevice));
     }
     vd::Geom gh = g, gs = g;
-    gh.nwhole = gs.nwhole = 0; gh.spec = gs.spec = nullptr;
+    gh.nwhole = gs.nwhole = 0;
     gh.nbatch = gs.nbatch = (uint32_t)steps;
     gh.inStride = strH; gs.inStride = strS; gh.outStride = gs.outStride = ostr;
     const unsigned gridB = 1600u * (unsigned)steps;
@@ -142,9 +136,7 @@ int main(int argc, char** argv)
         CK(hipStreamCreateWithFlags(&sb, hipStreamNonBlocking));
         hipEvent_t e0, e1, eb;
         CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1)); CK(hipEventCreate(&eb));
-        vd::Geom g2 = g;  // the second stream's split launches use their own vector slot
-        float* spec2; CK(hipMalloc(&spec2, 256 * vd::kSplitVecs * 64 * 4));
-        g2.spec = spec2;
+        vd::Geom g2 = g;
         void* out2; CK(hipMalloc(&out2, 16u << 20));
         std::vector<float> t1, t2;
         for (int r = 0; r < groups + 1; r++) {
@@ -174,7 +166,7 @@ int main(int argc, char** argv)
         hipEvent_t e0, e1, e2;
         CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1)); CK(hipEventCreate(&e2));
         vd::Geom gb = g;
-        gb.nwhole = 0; gb.spec = nullptr; gb.nbatch = (uint32_t)steps;
+        gb.nwhole = 0; gb.nbatch = (uint32_t)steps;
         const unsigned gridb = 1600u * (unsigned)steps;
         std::vector<float> th1, ts1, thb, tsb;
         for (int r = 0; r < groups + 1; r++) {

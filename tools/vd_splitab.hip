@@ -38,13 +38,12 @@ int main(int argc, char** argv)
     g.scale = 1.0f;
     CK(hipMalloc(&g.fair, vd::kFairBoardWords * 4));
     CK(hipMemset(g.fair, 0xFF, vd::kFairBoardWords * 4));
-    float* spec; uint32_t* stats;
-    CK(hipMalloc(&spec, 256 * vd::kSplitVecs * 64 * 4));
+    uint32_t* stats;
     CK(hipMalloc(&stats, 4));
     CK(hipMemset(stats, 0, 4));
     auto launch = [&](KFn f, bool split) {
         vd::Geom q = g;
-        if (split) { q.nwhole = 6144; q.spec = spec; q.stats = stats; }
+        if (split) { q.nwhole = 6144; q.stats = stats; }
         hipLaunchKernelGGL(f, dim3(split ? 1792 : 1600), dim3(256), 0, 0, in, out, q);
     };
     KFn f0 = (KFn)vd::vd_decode_tg<vd::HARD, vd::B32, 32, 0>, f32 = (KFn)vd::vd_decode_tg<vd::HARD, vd::B32, 32, 32>;
