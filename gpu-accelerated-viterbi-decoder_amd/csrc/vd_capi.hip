@@ -485,6 +485,23 @@ int vd_run_device_llr(vd_decoder* d, const float* llr_d, void* output_d, size_t 
     return launch_decode(d, llr_d, output_d, inputNum, (hipStream_t)stream, true, scale);
 }
 
+int vd_run_device_llr_batch(vd_decoder* d, const float* llr_d, size_t llr_stride, void* output_d, size_t output_stride,
+                            size_t inputNum, float scale, int nbatch, void* stream)
+{
+    if (!d || !llr_d || !output_d) return fail(VD_ERR_ARG, "null argument");
+    if (nbatch < 1) return fail(VD_ERR_ARG, "nbatch must be >= 1");
+    if (message_len(d->options, inputNum) == 0) return fail(VD_ERR_ARG, "inputNum too small");
+    if (nbatch > 1 && output_stride < message_len(d->options, inputNum) / 8)
+        return fail(VD_ERR_ARG, "output_stride smaller than the output size: batches would overlap");
+    if (nbatch > 1 && llr_stride < inputNum * sizeof(float) && llr_stride != 0)
+        return fail(VD_ERR_ARG, "llr_stride smaller than the input size: batches would overlap");
+    if ((uint64_t)vd::kChunks * (uint64_t)nbatch > 0xFFFFFFFFull) return fail(VD_ERR_ARG, "nbatch too large");
+    if ((llr_stride & 15) || (output_stride & 3)) return fail(VD_ERR_ARG, "llr_stride % 16 or output_stride % 4 != 0");
+    if (nbatch == 1) return launch_decode(d, llr_d, output_d, inputNum, (hipStream_t)stream, true, scale);
+    return launch_decode(d, llr_d, output_d, inputNum, (hipStream_t)stream, true, scale, (uint32_t)nbatch, llr_stride,
+                         output_stride);
+}
+
 int vd_run_llr(vd_decoder* d, const float* llr_h, void* output_h, size_t inputNum, float scale, float* kernel_ms)
 {
     if (!d || !llr_h || !output_h) return fail(VD_ERR_ARG, "null argument");

@@ -45,7 +45,7 @@ EXPORTS = ["vd_options_valid", "vd_input_size", "vd_message_len", "vd_output_siz
            "vd_simulate_host", "vd_count_errors", "vd_last_error", "vd_device_count", "vd_kernel_name",
            "vd_pack_device", "vd_run_device_llr", "vd_run_llr", "vd_host_alloc", "vd_host_free",
            "vd_run_stream", "vd_channel_device", "vd_simulate_device", "vd_mt_state_after", "vd_split_redecodes",
-           "vd_set_guard_check", "vd_guard_violations"]
+           "vd_set_guard_check", "vd_guard_violations", "vd_run_device_llr_batch"]
 
 
 class VitdecError(RuntimeError):
@@ -92,6 +92,7 @@ def lib():
     L.vd_run_stream.argtypes = [vp, ctypes.POINTER(vp), ctypes.POINTER(vp), i, sz, ctypes.POINTER(f)]
     L.vd_run_device_llr.argtypes = [vp, vp, vp, sz, f, vp]
     L.vd_run_llr.argtypes = [vp, vp, vp, sz, f, ctypes.POINTER(f)]
+    L.vd_run_device_llr_batch.argtypes = [vp, vp, sz, vp, sz, sz, f, ctypes.c_int, vp]
     L.vd_kernel_name.argtypes = [i]
     L.vd_kernel_name.restype = ctypes.c_char_p
     _lib = L
@@ -255,6 +256,12 @@ class ViterbiCUDA:
         """Async fused decode of inputNum device floats (16-byte aligned)."""
         _check(lib().vd_run_device_llr(self._h, ctypes.c_void_p(llr_ptr), ctypes.c_void_p(output_ptr), inputNum,
                                        scale, ctypes.c_void_p(stream)))
+
+    def run_device_llr_batch(self, llr_ptr, llr_stride, output_ptr, output_stride, inputNum, nbatch, scale=40000.0,
+                             stream=0):
+        """nbatch fused decodes of inputNum device floats each in one launch (vd_run_device_llr_batch)."""
+        _check(lib().vd_run_device_llr_batch(self._h, ctypes.c_void_p(llr_ptr), llr_stride, ctypes.c_void_p(output_ptr),
+                                             output_stride, inputNum, scale, nbatch, ctypes.c_void_p(stream)))
 
 
 class PinnedArray:

@@ -120,6 +120,11 @@ int vd_pack_device(int options, const float* llr_d, size_t inputNum, float scale
  * (no packed intermediate, one kernel), every format. */
 int vd_run_device_llr(vd_decoder* dec, const float* llr_d, void* output_d, size_t inputNum, float scale,
                       void* stream);
+/* nbatch independent batches of inputNum device floats in one launch (as vd_run_device_batch): batch b
+ * reads llr_d + b * llr_stride bytes and writes output_d + b * output_stride bytes (strides multiples
+ * of 16 and 4 bytes). */
+int vd_run_device_llr_batch(vd_decoder* dec, const float* llr_d, size_t llr_stride, void* output_d,
+                            size_t output_stride, size_t inputNum, float scale, int nbatch, void* stream);
 /* Blocking host-to-host variant (H2D of the floats, fused decode, D2H); kernel_ms as in vd_run. */
 int vd_run_llr(vd_decoder* dec, const float* llr_h, void* output_h, size_t inputNum, float scale, float* kernel_ms);
 

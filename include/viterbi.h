@@ -77,7 +77,9 @@ public:
     static constexpr int polyn1 = 0171;
     static constexpr int polyn2 = 0133;
 
+    // both overloads of the reference (viterbi.h:65-66)
     static constexpr int roundup(int a, int b) { return a <= 0 ? 0 : (a + b - 1) / b * b; }
+    static constexpr size_t roundup(size_t a, size_t b) { return a == 0 ? 0 : (a + b - 1) / b * b; }
     static constexpr int bitsPerMetric = metricType == M_B16 ? 16 : metricType == M_B32 ? 32 : 11;
     static constexpr int bitsPerPack = outputType == O_B16 ? 16 : 32;
     static constexpr int extraL_raw = 32;

@@ -94,3 +94,13 @@ def test_host_packer_matches_reference_quantiser_out_of_range(tmp_path, vo, ch):
     host_words = np.array([int(x) for x in r.stdout.split()], dtype=np.uint32)
     ref = vo.pack(ch, vals, scale=1.0).view(np.uint32)
     assert np.array_equal(host_words, ref)
+
+
+def test_viterbi_h_static_members_compile():
+    """include/viterbi.h has every static member and type the reference's callers use (main.cpp:121-128,137;
+    viterbiDF.h:176-180) and both roundup overloads (viterbi.h:65-66): static_asserts over every valid option"""
+    import subprocess
+    src = os.path.join(ROOT, "tests", "cxx", "viterbi_h_members.cpp")
+    r = subprocess.run(["g++", "-std=c++17", "-fsyntax-only", "-I", os.path.join(ROOT, "include"), src],
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr[-3000:]

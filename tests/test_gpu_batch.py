@@ -61,7 +61,8 @@ def test_batch_equals_single_runs(gpu, vo, opt, nbits):
 
 @pytest.mark.gpu
 def test_batch_with_input_stride_zero(gpu):
-    # the bench's timed region: every batch decodes the same resident input into its own output
+    # API edge case: input stride 0, every batch decodes the same input into its own output (the bench
+    # decodes distinct resident batches at a 256-byte-aligned stride instead)
     opt, nbits, nb = SOFT8 | M_B16, 32_000_000, 5
     n = 2 * nbits
     packed, stride, nin = _inputs(gpu, opt, nbits, 1)

@@ -116,3 +116,30 @@ def test_fused_llr_device_path_matches_host_path(gpu, vd):
         d.run_device_llr(v.data_ptr(), out.data_ptr(), vals.size, stream=torch.cuda.current_stream().cuda_stream)
         torch.cuda.synchronize()
     assert np.array_equal(out.cpu().numpy().view(np.uint32), host)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("opt", [HARD | M_B32, SOFT8 | M_B16, SOFT16 | M_B32, FP32 | M_FP16, SOFT4 | M_B16 | O_B16],
+                         ids=name)
+def test_fused_llr_batch_equals_single(gpu, vd, vo, opt):
+    """vd_run_device_llr_batch: 3 independent float batches in one launch, each equal to the oracle of its
+    own packed words; the bytes between the batches' outputs stay untouched"""
+    import torch
+    n, nb = 2 * 150_000, 3
+    vals = [channel_values(n, 0.5 + b, 21 + b) for b in range(nb)]
+    refs = [vo.decode(opt, vo.pack(opt, v, 40000.0), input_num=n)[0] for v in vals]
+    istride = (n * 4 + 255) // 256 * 256
+    nout = vd.lib().vd_output_size(opt, n)
+    ostride = (nout + 255) // 256 * 256 + 256
+    inp = torch.zeros(nb * istride // 4, dtype=torch.float32, device="cuda")
+    for b in range(nb):
+        inp[b * istride // 4: b * istride // 4 + n] = torch.from_numpy(vals[b]).cuda()
+    out = torch.full((nb * ostride,), 0xA5, dtype=torch.uint8, device="cuda")
+    with vd.ViterbiCUDA(opt) as d:
+        d.run_device_llr_batch(inp.data_ptr(), istride, out.data_ptr(), ostride, n, nb, 40000.0,
+                               torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+    for b in range(nb):
+        got = out[b * ostride: b * ostride + nout].cpu().numpy().view(refs[b].dtype)
+        np.testing.assert_array_equal(got, refs[b])
+        assert bool((out[b * ostride + nout: (b + 1) * ostride] == 0xA5).all())

@@ -19,7 +19,7 @@ import os
 import sys
 import time
 
-ROOT = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "gpu-accelerated-viterbi-decoder_amd"))
 
 import numpy as np  # noqa: E402
@@ -405,35 +405,11 @@ def llr_side_measurement(dev, sptr, stream, reps=20):
     t_pack, t_two, t_fused = timed(pack), timed(two), timed(fused)
     same = bool(torch.equal(out_fused, out_two))
     msg = vitdec.lib().vd_message_len(opt, n)
-    # as the timed region and other_configs: `reps` distinct float batches in one launch
-    # (vd_run_device_llr_batch); batch 0 is `vals`, the others fresh draws
-    istride = n * 4
-    many = torch.empty(reps * n, dtype=torch.float32, device=dev)
-    many[:n] = vals
-    for k in range(1, reps):
-        many[k * n:(k + 1) * n] = (torch.randint(0, 2, (n,), device=dev, generator=g).float() * 2 - 1
-                                   + 0.5 * torch.randn(n, device=dev, generator=g))
-    nout = out_fused.numel()
-    ostride = (nout + 255) // 256 * 256
-    outs = torch.empty(reps * ostride, dtype=torch.uint8, device=dev)
-    batched = lambda: dec.run_device_llr_batch(many.data_ptr(), istride, outs.data_ptr(), ostride, n, reps, 40000.0,
-                                               sptr)
-    settle(batched)
-    e = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
-    e[0].record(stream)
-    batched()
-    e[1].record(stream)
-    torch.cuda.synchronize()
-    t_batched = e[0].elapsed_time(e[1]) / reps
-    same_b = bool(torch.equal(outs[:nout], out_fused))
     dec.close()
-    del many, outs
     return {"workload": "64M float32 channel values (32M-bit SOFT8 batch, scale 40000) resident in HBM",
             "pack_ms": round(t_pack, 4), "pack_GBps": round(n * 4 / (t_pack * 1e-3) / 1e9, 1),
             "pack_then_decode_ms": round(t_two, 4), "fused_decode_ms": round(t_fused, 4),
-            "fused_gbps": round(msg / (t_fused * 1e-3) / 1e9, 2), "fused_equals_pack_then_decode": same,
-            "fused_batched": {"batches_per_launch": reps, "ms_per_batch": round(t_batched, 4),
-                              "gbps": round(msg / (t_batched * 1e-3) / 1e9, 2), "batch0_equals_single": same_b}}
+            "fused_gbps": round(msg / (t_fused * 1e-3) / 1e9, 2), "fused_equals_pack_then_decode": same}
 
 
 def channel_side_measurement(dev, sptr, reps=5, sample_bits=1_000_000):
@@ -547,7 +523,19 @@ def main():
         return ranks_check(world, rank)
     if torch.cuda.device_count() < world:
         sys.exit(f"bench.py: {world} ranks but only {torch.cuda.device_count()} visible GPU(s)")
-    init_ranks(world, local)
+    MODE = os.environ.get("PGMODE", "early")
+    if MODE == "early":
+        init_ranks(world, local)
+    elif MODE == "gloo":
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(free_port()), RANK="0", WORLD_SIZE="1", LOCAL_RANK="0")
+        torch.cuda.set_device(local)
+        torch.distributed.init_process_group("gloo")
+    elif MODE == "nodev":
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(free_port()), RANK="0", WORLD_SIZE="1", LOCAL_RANK="0")
+        torch.cuda.set_device(local)
+        torch.distributed.init_process_group("nccl")
+    else:
+        torch.cuda.set_device(local)
     dev = torch.cuda.current_device()
     stream = torch.cuda.current_stream()
     sptr = stream.cuda_stream
@@ -573,6 +561,8 @@ def main():
                             ostride=ostride, nout=nout, bits=bits, dec=dec, inp=inps[:nin], out=outs[:nout],
                             msg=vitdec.lib().vd_message_len(opt, input_num)))
     torch.cuda.synchronize()
+    if MODE == "late":
+        init_ranks(world, local)
 
     nw = len(batches)
     # The K steps are K independent batches per workload.  Each workload's batches go out as ONE launch
@@ -590,29 +580,14 @@ def main():
 
     # Warm-up: the W steps asked for, and at least WARM_S seconds of steps.  From idle the GPU takes
     # tens of milliseconds to reach its sustained clock; a timed region right behind a short warm-up read
-    # ~17 % slow kernels (0.221 vs 0.186 ms HARD, profiles/r02/clock_ramp.log).  So nothing may leave the
-    # GPU idle between the warm-up and the timed region: the first collective of a process (RCCL sets up
-    # its kernels there, ~20 ms) and the wait for ranks that finished input synthesis later run BEFORE
-    # the warm-up (one barrier), every rank then runs the same number of warm-up iterations (the max over
-    # ranks of what each needs), and the barrier in front of the timed region finds the ranks aligned.
-    # (With the set-up in that barrier the first timed launches ran on a cooled-down GPU: HARD 0.199 ms
-    # instead of 0.159 ms per batch, profiles/r03/README.md.)
-    torch.distributed.barrier()
-    torch.cuda.synchronize()
-
-    def warm_iteration():
+    # ~17 % slow kernels (0.221 vs 0.186 ms HARD, profiles/r02/clock_ramp.log).
+    nwarm = 0
+    tw = time.perf_counter()
+    while nwarm < args.warmup or time.perf_counter() - tw < args.warm_s:
         for b in batches:
             run(b)
+        nwarm += K
         torch.cuda.synchronize()
-
-    tw = time.perf_counter()
-    warm_iteration()
-    t_it = time.perf_counter() - tw
-    n_more = max(-(-args.warmup // K), int(np.ceil(args.warm_s / max(t_it, 1e-6)))) - 1
-    n_more = int(max_over_ranks(float(n_more), dev))
-    for _ in range(n_more):
-        warm_iteration()
-    nwarm = K * (1 + n_more)
     torch.distributed.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()

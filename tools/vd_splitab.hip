@@ -58,6 +58,18 @@ int main(int argc, char** argv)
         }
     for (int s = 0; s < 2; s++) { std::sort(t[s].begin(), t[s].end());
         printf("%-8s median %.4f ms  min %.4f ms\n", s ? "split" : "plain", t[s][t[s].size() / 2], t[s][0]); }
+    // back to back (the reference run()'s unit of work, one launch per batch, as a caller streams batches):
+    // per launch wall time between events around 20 launches, against the kernel span the clock stamps of
+    // single launches show below; the difference is the launch-to-launch gap
+    for (int s = 0; s < 2; s++) {
+        std::vector<float> tb;
+        for (int r = 0; r < rounds; r++) {
+            CK(hipEventRecord(e0)); for (int k = 0; k < 20; k++) launch(f0, s); CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
+            float ms; CK(hipEventElapsedTime(&ms, e0, e1)); tb.push_back(ms / 20);
+        }
+        std::sort(tb.begin(), tb.end());
+        printf("%-8s back to back (20 launches): median %.4f ms per launch\n", s ? "split" : "plain", tb[tb.size() / 2]);
+    }
     uint32_t redec = 0; CK(hipMemcpy(&redec, stats, 4, hipMemcpyDeviceToHost));
     printf("re-decoded split chunks over all split launches: %u\n", redec);
     for (int s = 0; s < 2; s++) {
