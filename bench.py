@@ -38,6 +38,15 @@ WORKLOADS = [
     ("hard_b32", vitdec.HARD | vitdec.M_B32 | vitdec.O_B32),
     ("soft8_b16", vitdec.SOFT8 | vitdec.M_B16 | vitdec.O_B32),
 ]
+# --workloads (profiling runs only, e.g. PMC passes over the other kernels; the default is the metric's
+# two): name -> (options, float channel values fused into the decode)
+ALL_WORKLOADS = {"hard_b32": (WORKLOADS[0][1], False), "soft8_b16": (WORKLOADS[1][1], False),
+                 "fp32_f16": (vitdec.FP32 | vitdec.M_FP16 | vitdec.O_B32, False),
+                 "soft4_b16": (vitdec.SOFT4 | vitdec.M_B16 | vitdec.O_B32, False),
+                 "soft16_b32": (vitdec.SOFT16 | vitdec.M_B32 | vitdec.O_B32, False),
+                 "hard_b32_ob16": (vitdec.HARD | vitdec.M_B32 | vitdec.O_B16, False),
+                 "soft8_b16_llr": (vitdec.SOFT8 | vitdec.M_B16 | vitdec.O_B32, True)}
+DEFAULT_WORKLOADS = ",".join(n for n, _ in WORKLOADS)
 
 
 def algorithmic_bytes(opt, input_num):
@@ -212,6 +221,19 @@ def resident_batches(opt, nbatch, seeds, dev, sptr):
         bs, ns = seeds(k)
         vitdec.simulate_device(opt, N_BITS, SNR_DB, bs, ns, bits[k].data_ptr(), inps[k * istride:].data_ptr(), sptr)
     return inps, istride, bits
+
+
+def resident_llr_batches(nbatch, seeds, dev, sptr):
+    """nbatch independent 32M-bit batches of float channel values (the reference's AddNoise output,
+    vd_channel_device: 64M floats each) resident in HBM, for the fused-quantisation decode"""
+    n = 2 * N_BITS
+    istride = (n * 4 + 255) // 256 * 256
+    vals = torch.empty(nbatch * istride // 4, dtype=torch.float32, device=dev)
+    bits = torch.empty(nbatch, N_BITS, dtype=torch.uint8, device=dev)
+    for k in range(nbatch):
+        bs, ns = seeds(k)
+        vitdec.channel_device(N_BITS, SNR_DB, bs, ns, bits[k].data_ptr(), vals.data_ptr() + k * istride, sptr)
+    return vals.view(torch.uint8), istride, bits
 
 
 def batch_ber(opt, bits, outs, ostride, nout, k, msg):
@@ -527,6 +549,8 @@ def main():
     ap.add_argument("--no-pcie", action="store_true", help="skip the host-to-host pipelined side measurement")
     ap.add_argument("--no-channel", action="store_true", help="skip the channel-source side measurement")
     ap.add_argument("--no-other", action="store_true", help="skip the other-formats side measurement")
+    ap.add_argument("--workloads", default=DEFAULT_WORKLOADS,
+                    help="profiling runs only: comma-separated workloads to time (" + ",".join(ALL_WORKLOADS) + ")")
     ap.add_argument("--ranks-check", action="store_true", help=argparse.SUPPRESS)  # tests: rank layout only
     args = ap.parse_args()
 
@@ -560,16 +584,25 @@ def main():
     P = min(K, POOL)
     sizes = [P] * (K // P) + ([K % P] if K % P else [])  # batches per launch
     batches = []
-    for wi, (name, opt) in enumerate(WORKLOADS):
+    names = args.workloads.split(",")
+    if any(n not in ALL_WORKLOADS for n in names):
+        sys.exit(f"bench.py: unknown workload in {args.workloads} (known: {', '.join(ALL_WORKLOADS)})")
+    metric_run = args.workloads == DEFAULT_WORKLOADS
+    for wi, name in enumerate(names):
+        opt, llr = ALL_WORKLOADS[name]
         input_num = 2 * N_BITS
         nout = vitdec.lib().vd_output_size(opt, input_num)
-        inps, istride, bits = resident_batches(opt, P, lambda k: rank_seed(rank, wi, k, world), dev, sptr)
+        seeds = lambda k: rank_seed(rank, wi, k, world)
+        if llr:
+            inps, istride, bits = resident_llr_batches(P, seeds, dev, sptr)
+        else:
+            inps, istride, bits = resident_batches(opt, P, seeds, dev, sptr)
         ostride = (nout + 255) // 256 * 256
         outs = torch.empty(P * ostride, dtype=torch.uint8, device=dev)  # one output per resident batch
         dec = vitdec.ViterbiCUDA(opt, 0, dev)
         nin = vitdec.lib().vd_input_size(opt, input_num)
         # inp / out: batch 0 (the step the CPU baseline and the PCIe side measurement repeat)
-        batches.append(dict(name=name, opt=opt, input_num=input_num, inps=inps, istride=istride, outs=outs,
+        batches.append(dict(name=name, opt=opt, llr=llr, input_num=input_num, inps=inps, istride=istride, outs=outs,
                             ostride=ostride, nout=nout, bits=bits, dec=dec, inp=inps[:nin], out=outs[:nout],
                             msg=vitdec.lib().vd_message_len(opt, input_num)))
     torch.cuda.synchronize()
@@ -585,8 +618,12 @@ def main():
 
     def run(b):
         for nbatch in sizes:
-            b["dec"].run_device_batch(b["inps"].data_ptr(), b["istride"], b["outs"].data_ptr(), b["ostride"],
-                                      b["input_num"], nbatch, sptr)
+            if b["llr"]:
+                b["dec"].run_device_llr_batch(b["inps"].data_ptr(), b["istride"], b["outs"].data_ptr(), b["ostride"],
+                                              b["input_num"], nbatch, 40000.0, sptr)
+            else:
+                b["dec"].run_device_batch(b["inps"].data_ptr(), b["istride"], b["outs"].data_ptr(), b["ostride"],
+                                          b["input_num"], nbatch, sptr)
 
     # Warm-up: the W steps asked for, and at least WARM_S seconds of steps.  From idle the GPU takes
     # tens of milliseconds to reach its sustained clock; a timed region right behind a short warm-up read
@@ -644,11 +681,12 @@ def main():
                 sums0.append(x)
         bers.append(max(ber_k))
         sums.append(ck)
-    llr = None if (args.no_llr or rank != 0) else llr_side_measurement(dev, sptr, stream)
-    pcie = None if (args.no_pcie or rank != 0) else pcie_side_measurement(batches, dev)
-    chan = None if (args.no_channel or rank != 0) else channel_side_measurement(dev, sptr)
-    other = None if (args.no_other or rank != 0) else other_configs_side_measurement(dev, sptr, stream)
-    single = None if (args.no_other or rank != 0) else single_launch_side_measurement(batches, stream, sptr)
+    side = rank == 0 and metric_run
+    llr = None if (args.no_llr or not side) else llr_side_measurement(dev, sptr, stream)
+    pcie = None if (args.no_pcie or not side) else pcie_side_measurement(batches, dev)
+    chan = None if (args.no_channel or not side) else channel_side_measurement(dev, sptr)
+    other = None if (args.no_other or not side) else other_configs_side_measurement(dev, sptr, stream)
+    single = None if (args.no_other or not side) else single_launch_side_measurement(batches, stream, sptr)
     # the same collectives at every N (N = 1: a 1-rank RCCL group)
     elapsed = max_over_ranks(elapsed, dev)
     gathered = gather_checksums(sums + sums0, dev, world)
@@ -676,7 +714,8 @@ def main():
 
         def kernel_roofline(i):
             b = batches[i]
-            alg = algorithmic_bytes(b["opt"], b["input_num"])
+            alg = algorithmic_bytes(b["opt"], b["input_num"]) if not b["llr"] else \
+                4 * b["input_num"] + vitdec.lib().vd_output_size(b["opt"], b["input_num"])
             ach = alg / (kms[i] * 1e-3) / 1e9
             pmc = pmcs.get(b["name"], {})
             stages = stages_per_launch(b["opt"], b["input_num"])
@@ -766,7 +805,9 @@ def main():
             result["config"]["single_launch"] = single
         if final_gather is not None:
             result["config"]["final_gather"] = final_gather
-        if not args.no_cpu_baseline and world == 1:
+        if not metric_run:
+            result["config"]["profiling_workloads"] = names
+        if not args.no_cpu_baseline and world == 1 and metric_run:
             result["cpu_baseline"] = cpu_baseline(batches)
         print(json.dumps(result), flush=True)
 

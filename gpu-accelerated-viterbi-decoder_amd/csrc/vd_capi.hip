@@ -24,6 +24,7 @@
 #include "vd_pack.h"
 #include "vd_mt.h"
 #include "vd_mtjump.h"
+#include "vd_segplan.h"
 
 namespace {
 
@@ -95,22 +96,20 @@ uint64_t avail_stages(int o, size_t n)
     return per < half ? per : half;
 }
 
-using launch_fn = void (*)(const void*, void*, vd::Geom, hipStream_t);
+using launch_fn = void (*)(const void*, void*, vd::Geom, unsigned, hipStream_t);
 
-// workgroups of a launch: whole-chunk workgroups plus one per split chunk
+// workgroups of a launch without a segment table: one chunk per wave
 unsigned tg_grid(const vd::Geom& g)
 {
-    if (g.nbatch > 1) return (unsigned)(((uint64_t)g.nchunks * g.nbatch + vd::kWaves - 1) / vd::kWaves);
-    if (g.nwhole == 0) return (g.nchunks + vd::kWaves - 1) / vd::kWaves;
-    return g.nwhole / vd::kWaves + (g.nchunks - g.nwhole);
+    return (unsigned)(((uint64_t)g.nchunks * g.nbatch + vd::kWaves - 1) / vd::kWaves);
 }
 
 // one kernel per format (SOFT16 on int32 patterns, TgFmt::INT); CH >= kLlr: float channel values
 // quantised in the table build (fused SoftDecisionPacker)
 template <int CH, int CORE, int OB>
-void launch_t(const void* in, void* out, vd::Geom g, hipStream_t s)
+void launch_t(const void* in, void* out, vd::Geom g, unsigned grid, hipStream_t s)
 {
-    hipLaunchKernelGGL((vd::vd_decode_tg<CH, CORE, OB>), dim3(tg_grid(g)), dim3(64 * vd::kWaves), 0, s, in, out, g);
+    hipLaunchKernelGGL((vd::vd_decode_tg<CH, CORE, OB>), dim3(grid), dim3(64 * vd::kWaves), 0, s, in, out, g);
 }
 
 template <int CH, int CORE>
@@ -180,8 +179,8 @@ struct vd_decoder {
     void* out2_d = nullptr;
     size_t cap2_in = 0, cap2_out = 0;
     hipStream_t s_in = nullptr, s_out = nullptr;
-    DeviceState* ds = nullptr;  // the device's board / split state (looked up once, vd_create)
-    bool split = true;          // split launches allowed (VD_NO_SPLIT=1 at vd_create: no)
+    DeviceState* ds = nullptr;  // the device's board / segment tables (looked up once, vd_create)
+    int split = 1;              // segment launches: 0 none (VD_NO_SPLIT=1), 1 pieces, 2 thirds (VD_SPLIT=...)
     uint32_t* check = nullptr;  // LDS guard violation counter (vd_set_guard_check), null = off
 };
 
@@ -208,13 +207,19 @@ static int ensure_capacity(vd_decoder* d, size_t inBytes, size_t outBytes)
 //  * the progress board of the decode kernels' fairness controller (vd_kernels.h Fair, Geom::fair),
 //    every word kFairEmpty at rest (the kernels free their slots); concurrent launches sharing it only
 //    perturb issue priorities;
-//  * the re-decode counter of split launches (vd_split_redecodes).
-// Split launches keep their boundary vectors in LDS (vd_kernel_tg.h "split chunks"), so launches on any
-// number of streams share no scratch.  A decoder looks the state up once (vd_create), not per launch.
+//  * the segment tables of segment launches (read only; vd_kernel_tg.h "segment launches");
+//  * the re-decode counter of segment launches (vd_split_redecodes).
+// Segment launches keep their boundary vectors in LDS, so launches on any number of streams share no
+// scratch.  A decoder looks the state up once (vd_create), not per launch.
+struct SegTable {
+    uint32_t* d = nullptr;  // first chunk of each workgroup, then the chunk count
+    unsigned nwg = 0;
+};
 struct DeviceState {
     uint32_t* board = nullptr;
     int nsimd = 0;
     uint32_t* stats = nullptr;
+    SegTable pieces, thirds;
 };
 static DeviceState* device_state(int device)
 {
@@ -228,10 +233,18 @@ static DeviceState* device_state(int device)
             return nullptr;
         DeviceState* x = new DeviceState;
         x->nsimd = 4 * cus;
-        if (hipMalloc(&x->board, vd::kFairBoardWords * 4) != hipSuccess ||
-            hipMemset(x->board, 0xFF, vd::kFairBoardWords * 4) != hipSuccess ||
-            hipMalloc(&x->stats, 4) != hipSuccess || hipMemset(x->stats, 0, 4) != hipSuccess ||
-            hipDeviceSynchronize() != hipSuccess) {
+        bool ok = hipMalloc(&x->board, vd::kFairBoardWords * 4) == hipSuccess &&
+                  hipMemset(x->board, 0xFF, vd::kFairBoardWords * 4) == hipSuccess &&
+                  hipMalloc(&x->stats, 4) == hipSuccess && hipMemset(x->stats, 0, 4) == hipSuccess;
+        for (int th = 0; th < 2 && ok; th++) {
+            const std::vector<uint32_t> t = vd::seg_table(x->nsimd, th == 1);
+            if (t.empty()) continue;
+            SegTable& T = th ? x->thirds : x->pieces;
+            ok = hipMalloc(&T.d, t.size() * 4) == hipSuccess &&
+                 hipMemcpy(T.d, t.data(), t.size() * 4, hipMemcpyHostToDevice) == hipSuccess;
+            T.nwg = (unsigned)(t.size() - 1);
+        }
+        if (!ok || hipDeviceSynchronize() != hipSuccess) {
             delete x;
             return nullptr;
         }
@@ -239,17 +252,17 @@ static DeviceState* device_state(int device)
     }
     return st[device];
 }
-// Split the launch when the whole chunks leave exactly one piece wave per SIMD (6400 chunks on 1024
-// SIMDs: 6 whole chunks per SIMD + 256 chunks in 4 pieces) and the chunks are long enough.
-static void plan_split(vd::Geom& g, int options, const DeviceState* x)
+// Segment launch when the chunks are long enough and the device has a table; returns the grid
+static unsigned plan_split(vd::Geom& g, int options, const DeviceState* x, int mode)
 {
     const uint64_t words32 = out_of(options) != 0 ? g.packNum / 2 : g.packNum;  // O_B16: 16-bit words
-    if (words32 / g.nchunks < (uint64_t)vd::kSplitMinWords) return;
-    const uint32_t nsimd = (uint32_t)x->nsimd;
-    const uint32_t perSimd = g.nchunks / nsimd, rem = g.nchunks % nsimd, nwhole = g.nchunks - rem;
-    if (rem == 0 || rem * vd::kWaves != nsimd || perSimd + 1 > 8) return;  // 8 waves per SIMD (vd_kernel_tg.h kTbs)
-    g.nwhole = nwhole;
+    if (mode == 0 || g.nchunks != (uint32_t)vd::kChunks || words32 / g.nchunks < (uint64_t)vd::kSplitMinWords)
+        return tg_grid(g);
+    const SegTable& T = mode == 2 && x->thirds.d ? x->thirds : x->pieces;
+    if (!T.d) return tg_grid(g);
+    g.seg = T.d;
     g.stats = x->stats;
+    return T.nwg;
 }
 
 // llr: in_d holds inputNum float channel values, quantised in the kernel (scale = packer scale).
@@ -281,8 +294,8 @@ static int launch_decode(const vd_decoder* d, const void* in_d, void* out_d, siz
     g.nbatch = nbatch;
     g.inStride = inStride;
     g.outStride = outStride;
-    if (d->split && nbatch == 1) plan_split(g, options, d->ds);
-    f(in_d, out_d, g, s);
+    const unsigned grid = nbatch == 1 ? plan_split(g, options, d->ds, d->split) : tg_grid(g);
+    f(in_d, out_d, g, grid, s);
     VD_HIP(hipGetLastError());
     return VD_OK;
 }
@@ -333,7 +346,8 @@ int vd_create(int options, size_t preallocInputNum, int device, vd_decoder** out
         return fail(VD_ERR_NOMEM, "per-device decode state allocation failed");
     }
     const char* nosplit = std::getenv("VD_NO_SPLIT");
-    d->split = !(nosplit && nosplit[0] == '1');
+    const char* smode = std::getenv("VD_SPLIT");
+    d->split = nosplit && nosplit[0] == '1' ? 0 : smode && !strcmp(smode, "thirds") ? 2 : 1;
     const char* chk = std::getenv("VD_CHECK");
     if (chk && chk[0] == '1') {
         int rc = vd_set_guard_check(d, 1);

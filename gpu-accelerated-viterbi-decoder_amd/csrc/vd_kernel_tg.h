@@ -44,6 +44,8 @@ constexpr int kLlr = 8;
 // vd_decode_tg is a set of these bits, 0 in the product.
 constexpr int kAblNoTraceback = 1, kAblNoTabReads = 2, kAblNoReadout = 4, kAblNoTabBuild = 8, kAblNoLoads = 16,
               kAblClock = 32, kAblNoFair = 256, kAblNoTabWrites = 512, kAblNoGuardSpace = 1024;
+// layout variants (tools A/B; exact twins of the product)
+constexpr int kAblRowTable = 2048;  // fp32 cores: the interleaved-row table (TgTab) written with ds_write2_b32
 constexpr int kAblAcsOnly = kAblNoTraceback | kAblNoTabReads | kAblNoReadout | kAblNoTabBuild | kAblNoLoads;
 
 template <int CH>
@@ -65,7 +67,7 @@ struct TgFmt {
 // fits, so |V +- E| < 2^31.  The CLI default SNR 15 (saturated soft values on the codeword: the best
 // path gains BMmax every stage) is in the parity tests; tests/test_metric_range.py checks the bounds.
 
-// Branch-metric table: per 96-stage group, 16 periods of 6 rows (row K = stage phase); a row holds
+// Interleaved-row table (SOFT16; the fp32 cores use TgTabL below): per 96-stage group, 16 periods of 6 rows (row K = stage phase); a row holds
 // E[L] = BM[L]*2^S + tag for the four labels L.  Rows K of periods 2m and 2m+1 are interleaved entry by
 // entry, so a lane's entries for stages t and t+6 are one 8-byte ds_read_b64: entry e of row r sits at
 // row(r) + 8e.  The SOFT16 (INT, M_B32) phase-0 rows hold, per label, the pair (E-, E+) of both tag
@@ -86,15 +88,50 @@ struct TgTab {
     }
     static constexpr int BYTES = 8 * 60 * 4;
 };
+// Label-region table (the fp32 cores' table): one region of 96 entries per label, entry of stage
+// t = 12m + 6o + K (period pair m, period o, phase K) at index 12m + 2K + o, so the entries of stages t and
+// t+6 (o = 0, 1) are one ds_read_b64; the regions are 104 dwords apart (banks 0, 40, 16, 56: the four
+// labels' reads in a lane group never share a bank).  Lane l builds the entries of the stage at index l
+// (and lanes 0..31 index 64 + l) and writes them with ds_write_addtid_b32 (address = M0 + offset + 4 lane,
+// no address VGPR: 2 cycles of the store path per 256 B instead of 6 per 512 B for ds_write2_b32 at
+// scattered row addresses).  Against the interleaved-row table (TgTab, kAblRowTable): HARD 0.1627 ->
+// 0.1582 ms, SOFT8 0.1655 -> 0.1632 ms per batch under bench conditions, exact twins
+// (profiles/r03/benchab_label_regions.log).
+struct TgTabL {
+    static constexpr int REGION = 104 * 4;  // bytes per label region
+    static __host__ __device__ constexpr bool pairrow(int) { return false; }
+    static __host__ __device__ constexpr int index(int r) { return 12 * (r / 12) + 2 * (r % 6) + (r / 6) % 2; }
+    static __host__ __device__ constexpr int row(int r) { return 4 * index(r); }
+    // stage (within the group) whose entries table index i holds
+    static __host__ __device__ constexpr int stage(int i) { return 12 * (i / 12) + 6 * (i % 2) + (i % 12) / 2; }
+    static constexpr int BYTES = 4 * REGION;
+};
+static_assert(TgTabL::stage(TgTabL::index(95)) == 95 && TgTabL::index(TgTabL::stage(64)) == 64, "index <-> stage");
+// ds_write_addtid_b32 x4: LDS[M0 + OFF + k R + 4 lane] = v_k for the active lanes.  M0 is a register the
+// compiler reserves (it does not honour an "m0" clobber), so the statement saves and restores it.
+template <int OFF, int R>
+__device__ __forceinline__ void lds_write_addtid4(uint32_t base, float v0, float v1, float v2, float v3)
+{
+    uint32_t t;
+    asm volatile("s_mov_b32 %[t], m0\n\ts_mov_b32 m0, %[b]\n\ts_nop 0\n\t"
+                 "ds_write_addtid_b32 %[v0] offset:%[o0]\n\tds_write_addtid_b32 %[v1] offset:%[o1]\n\t"
+                 "ds_write_addtid_b32 %[v2] offset:%[o2]\n\tds_write_addtid_b32 %[v3] offset:%[o3]\n\t"
+                 "s_mov_b32 m0, %[t]"
+                 : [t] "=&s"(t)
+                 : [b] "s"(base), [v0] "v"(v0), [v1] "v"(v1), [v2] "v"(v2), [v3] "v"(v3), [o0] "i"(OFF),
+                   [o1] "i"(OFF + R), [o2] "i"(OFF + 2 * R), [o3] "i"(OFF + 3 * R)
+                 : "memory");
+}
+
 // Survivor ring slots per wave minus one (words traced per traceback batch): table + ring + guards of 4
-// waves (20,160 B) fit 8 workgroups per CU, so every SIMD holds 8 waves (<= 64 VGPRs): 1.4 % faster per
+// waves (19,136 B; SOFT16 20,160 B) fit 8 workgroups per CU, so every SIMD holds 8 waves (<= 64 VGPRs): 1.4 % faster per
 // batch than 13 slots at 7 waves (profiles/r02/benchab_8w.log), the shorter traceback batches included.
 constexpr int kTbs = 11;
 constexpr int kGuardWords = 4;                 // guard words before the table, between table and ring, after the ring
 constexpr uint32_t kGuardPattern = 0xA5C3E10Fu;
-template <bool PAIR0, int GW = kGuardWords>
+template <int TABB, int GW = kGuardWords>
 struct TgLds {
-    static constexpr int TAB = TgTab<PAIR0>::BYTES / 4;     // table words
+    static constexpr int TAB = TABB / 4;                   // table words
     static constexpr int RING = (kTbs + 1) * 64;           // ring words
     static constexpr int TAB_OFF = GW;                     // word offsets within a wave's part
     static constexpr int RING_OFF = 2 * GW + TAB;
@@ -105,7 +142,7 @@ struct TgLds {
         return i < GW ? i : i < 2 * GW ? TAB + i : TAB + RING + i;
     }
 };
-static_assert(kWaves * TgLds<false>::WAVE * 4 <= 20480 && kWaves * TgLds<true>::WAVE * 4 <= 20480,
+static_assert(kWaves * TgLds<TgTab<false>::BYTES>::WAVE * 4 <= 20480 && kWaves * TgLds<TgTab<true>::BYTES>::WAVE * 4 <= 20480,
               "8 workgroups of 4 waves per CU (160 KiB of LDS)");
 
 __device__ __forceinline__ int tg_pos(int l)
@@ -449,52 +486,83 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t tg_rsrc(const void* in, uint64
     return __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)in + off), (short)0, (int)lo, 0x00020000);
 }
 
-// ---------------------------------------------------------------- split chunks
-// A launch of 6400 chunks on 1024 SIMDs puts 7 waves on a quarter of the SIMDs and 6 on the rest; the
-// 7-wave SIMDs set the kernel time.  In a split launch (Geom::nwhole) the first nwhole chunks are
-// decoded whole, one per wave, and each remaining chunk by one workgroup as kWaves pieces, so every
-// SIMD gets 6 whole chunks and one piece.  Piece 0 starts at the chunk start (exact).  Piece q > 0
-// starts kSplitWarm blocks before its first word's emit block from equal metrics; at that boundary
-// block it records its renormalised metric vector (its start vector), and piece q-1 records its own
-// vector at the same block (its end vector).  Equal vectors mean every later decision of piece q equals
-// the exact decode's (the recursion and the tie rules depend only on metric differences; V at a block
-// start is VBASE + (metric - metric of position 0) * 2^S with cleared fields), so piece q is verified
-// when piece q-1 is and the two vectors agree.  After each pass every piece that ran publishes its two
-// vectors in its own (now dead) table LDS, the workgroup synchronises (s_barrier) and every wave
-// evaluates the same checks.  Each unverified piece takes its left neighbour's end vector into a register,
-// a second barrier lets everyone finish reading, and the unverified pieces re-decode their words from
-// their boundary blocks.  The first unverified piece always restarts from an exact vector, so every pass
-// verifies at least one more piece: at most kWaves - 1 re-decode passes, no timeouts, no flags.  Writes of
-// a later pass follow the barriers, so the last (verified) decode of every word is the one that stays.
-// Block boundaries are multiples of 3 (the group length, 96 stages = 16 trellis periods) so every run
-// uses the same position <-> state map there.  The vectors never leave the workgroup's LDS, so
-// concurrent split launches share no storage.
-constexpr int kSplitWarm = 6;                // warm-up blocks of a speculative piece (multiple of 3)
+// ---------------------------------------------------------------- segment launches
+// A launch of 6400 chunks on 1024 SIMDs, one chunk per wave, puts 7 waves on a quarter of the SIMDs and
+// 6 on the rest, and the 7-wave SIMDs set the kernel time.  In a segment launch (Geom::seg) workgroup g
+// decodes the consecutive chunks [seg[g], seg[g+1]) as kWaves segments of about equal length, one per
+// wave; a segment may end in one chunk and continue at the start of the next (each chunk part is a
+// "run").  A segment that starts at a chunk start is exact.  One that starts inside a chunk starts
+// kSplitWarm blocks before its first word's emit block from equal metrics; at that boundary block it
+// records its renormalised metric vector (its start vector), and the segment to its left records its own
+// vector at the same block (its end vector).  Equal vectors mean every later decision of the segment
+// equals the exact decode's (the recursion and the tie rules depend only on metric differences; V at a
+// block start is VBASE + (metric - metric of position 0) * 2^S with cleared fields), so a segment is
+// verified when its left neighbour is and the two vectors agree.  After each pass every segment that ran
+// publishes its two vectors in its own (now dead) table LDS, the workgroup synchronises (s_barrier) and
+// every wave evaluates the same checks.  Each unverified segment takes its left neighbour's end vector
+// into a register, a second barrier lets everyone finish reading, and the unverified segments re-decode
+// their first run from its boundary block (their later runs start at chunk starts and are exact).  The
+// first unverified segment always restarts from an exact vector, so every pass verifies at least one
+// more: at most kWaves - 1 re-decode passes, no timeouts, no flags.  Writes of a later pass follow the
+// barriers, so the last (verified) decode of every word is the one that stays.  Block boundaries inside
+// a chunk are multiples of 3 (the group length, 96 stages = 16 trellis periods) so every run uses the
+// same position <-> state map there.  The vectors never leave the workgroup's LDS, so concurrent launches
+// share no storage.  The host's tables (vd_capi.hip plan_split): 256 workgroups of one chunk in 4 pieces
+// after 1536 of 4 whole chunks (7 waves per SIMD, round 2's split), or 1792 workgroups of 3 chunks and
+// 256 of 4 (8 waves of 3/4 chunk or 1 chunk per SIMD, their progress kept even by the fairness controller
+// in fractions of their work).
+constexpr int kSplitWarm = 6;                // warm-up blocks of a speculative segment (multiple of 3)
 constexpr int kSplitMinWords = 64;           // chunks of fewer 32-bit words are not split (host side)
-struct SplitGeo {
+constexpr int kSegSnap = 8;                  // a boundary this close to a chunk start or end moves onto it
+// a workgroup's chunks (at most kWaves) and their 32-bit word counts; wave-uniform, in scalar registers
+struct SegWG {
+    uint32_t c0;
+    int k;
+    uint32_t W0, W1, W2, W3;
+    __device__ __forceinline__ uint32_t W(int i) const { return i == 0 ? W0 : i == 1 ? W1 : i == 2 ? W2 : W3; }
+    __device__ __forceinline__ uint32_t cum(int i) const  // words of chunks 0 .. i-1
+    {
+        return (i > 0 ? W0 : 0u) + (i > 1 ? W1 : 0u) + (i > 2 ? W2 : 0u) + (i > 3 ? W3 : 0u);
+    }
+};
+struct SegPos {
+    int i;       // chunk within the workgroup (k: the end)
+    uint32_t a;  // local word; a > 0: (a + 1) % 3 == 0 and a >= kSplitWarm
+};
+// boundary q (0 .. kWaves) of the workgroup's segments
+__device__ __forceinline__ SegPos seg_bound(const SegWG& w, int q)
+{
+    if (q == 0) return {0, 0u};
+    if (q == kWaves) return {w.k, 0u};
+    const uint32_t x = (uint32_t)q * w.cum(w.k) / kWaves;
+    int i = 0;
+    while (i + 1 < w.k && w.cum(i + 1) <= x) i++;
+    const uint32_t a = x - w.cum(i);
+    if (a < kSegSnap) return {i, 0u};
+    if (w.W(i) - a < kSegSnap) return {i + 1, 0u};
+    return {i, a - (a + 1) % 3};
+}
+// one run: chunk c0 + i, frame word 0 = chunk word s0, emits words [E, words) of the frame; Xspec / Xcmp:
+// the frame blocks of its left / right boundary (-1: none)
+struct RunGeo {
+    int i;
     uint32_t s0, words, E;
     int Xspec, Xcmp;
 };
-// boundary word of piece q (q = 1 .. kWaves-1): (k + 1) % 3 == 0, so the boundary block k + 1 starts a group
-__device__ __forceinline__ uint32_t split_bound(uint32_t Sc, int q)
+__device__ __forceinline__ RunGeo seg_run(const SegWG& w, SegPos b0, SegPos b1, int r)
 {
-    const uint32_t k = (uint32_t)q * Sc / kWaves;
-    return k - (k + 1) % 3;
-}
-// piece q's frame: local word 0 = chunk word s0; it emits words [E, words) of the frame; Xspec / Xcmp:
-// the local blocks of its left / right boundary (-1: none)
-__device__ __forceinline__ SplitGeo split_geo(uint32_t Sc, int q)
-{
-    SplitGeo g;
-    const uint32_t kq = q == 0 ? 0 : split_bound(Sc, q);
-    const uint32_t kn = q == kWaves - 1 ? Sc : split_bound(Sc, q + 1);
-    g.s0 = q == 0 ? 0 : kq + 1 - kSplitWarm;
-    g.words = kn - g.s0;
-    g.E = kq - g.s0;
-    g.Xspec = q == 0 ? -1 : (int)(kq + 1 - g.s0);
-    g.Xcmp = q == kWaves - 1 ? -1 : (int)(kn + 1 - g.s0);
+    RunGeo g;
+    g.i = b0.i + r;
+    const uint32_t a = r == 0 ? b0.a : 0u, W = w.W(g.i);
+    const uint32_t b = g.i == b1.i ? b1.a : W;
+    g.s0 = a == 0 ? 0u : a + 1 - kSplitWarm;
+    g.words = b - g.s0;
+    g.E = a - g.s0;
+    g.Xspec = a == 0 ? -1 : (int)(a + 1 - g.s0);
+    g.Xcmp = b == W ? -1 : (int)(b + 1 - g.s0);
     return g;
 }
+__device__ __forceinline__ int seg_nruns(SegPos b0, SegPos b1) { return b1.i - b0.i + (b1.a != 0 ? 1 : 0); }
 
 // ================================================================ the kernel: one chunk per wave
 template <int CH, int CORE, int OB, int ABL = 0>
@@ -511,8 +579,10 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(8))
     // s = -1 in the upper half (v_fma, as cheap as v_add), and the M_B32 table is the M_B16 one.  SOFT16
     // (INT) keeps the pair rows: each lane reads its own tag sign's half.
     constexpr bool S32 = CORE == B32 && !INT;
-    using TT = TgTab<INT>;
-    using LL = TgLds<INT, (ABL & kAblNoGuardSpace) ? 0 : kGuardWords>;
+    // LR: the label-region table (TgTabL) written with ds_write_addtid_b32 (SOFT16 keeps the pair-row table)
+    constexpr bool LR = !INT && !(ABL & kAblRowTable);
+    using TT = std::conditional_t<LR, TgTabL, TgTab<INT>>;
+    using LL = TgLds<TT::BYTES, (ABL & kAblNoGuardSpace) ? 0 : kGuardWords>;
     constexpr int J = FMT::J, S = FMT::S;
     __shared__ __attribute__((aligned(16))) uint32_t lds[kWaves * LL::WAVE];
     const int lane = threadIdx.x & 63;
@@ -521,32 +591,51 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(8))
     uint32_t* const wlds = lds + wv * LL::WAVE;
     char* const tabb = (char*)(wlds + LL::TAB_OFF);
     uint32_t* const ring = wlds + LL::RING_OFF;
-    // This wave's work: chunk blockIdx.x * kWaves + wv, or, in a split launch (Geom::nwhole), piece wv of
-    // chunk nwhole + (blockIdx.x - nwhole / kWaves) -- see "split chunks" above.
+    // This wave's work: chunk blockIdx.x * kWaves + wv, or, in a segment launch (Geom::seg), segment wv of
+    // the workgroup's chunks -- see "segment launches" above.
     // A batched launch (Geom::nbatch > 1) decodes chunk c of batch b at launch chunk b * nchunks + c.
-    const bool split = geo.nwhole != 0 && blockIdx.x >= geo.nwhole / kWaves;
-    const uint32_t gchunk = split ? geo.nwhole + (blockIdx.x - geo.nwhole / kWaves) : blockIdx.x * kWaves + wv;
-    const uint32_t batch = geo.nbatch > 1 ? gchunk / geo.nchunks : 0u;
-    const uint32_t chunk = gchunk - batch * geo.nchunks;
+    const bool split = geo.seg != nullptr;
+    const int piece = split ? wv : -1;
+    const uint32_t gchunk = blockIdx.x * kWaves + wv;
+    const uint32_t batch = geo.nbatch > 1 && !split ? gchunk / geo.nchunks : 0u;
     const void* const in = (const char*)in_all + batch * geo.inStride;
     void* const out = (char*)out_all + batch * geo.outStride;
-    const int piece = split ? wv : -1;
-    const ChunkRange cr = chunk_range(geo, chunk);
-    if (cr.words == 0) return;  // never in a split workgroup: split chunks have >= kSplitMinWords words
+    auto words32 = [&](uint32_t c) {  // 32-bit words traced back in chunk c
+        const uint32_t w = chunk_range(geo, c).words;
+        return OB == 32 ? w : (w + 1) / 2;
+    };
+    SegWG sw;
+    if (split) {
+        sw.c0 = geo.seg[blockIdx.x];
+        sw.k = (int)(geo.seg[blockIdx.x + 1] - sw.c0);
+        sw.W0 = words32(sw.c0);
+        sw.W1 = sw.k > 1 ? words32(sw.c0 + 1) : 0u;
+        sw.W2 = sw.k > 2 ? words32(sw.c0 + 2) : 0u;
+        sw.W3 = sw.k > 3 ? words32(sw.c0 + 3) : 0u;
+    } else {
+        sw.c0 = gchunk - batch * geo.nchunks;
+        sw.k = 1;
+        sw.W0 = words32(sw.c0);
+        sw.W1 = sw.W2 = sw.W3 = 0u;
+        if (sw.W0 == 0) return;  // an empty chunk (never in a segment launch: its chunks have >= kSplitMinWords words)
+    }
+    // this wave's segment [b0, b1) and the segments whose start is exact (a chunk start)
+    const SegPos b0 = split ? seg_bound(sw, wv) : SegPos{0, 0u}, b1 = split ? seg_bound(sw, wv + 1) : SegPos{1, 0u};
+    const int nrun = seg_nruns(b0, b1);
     // guard words (Geom::check): a uniform branch, nothing when off
     if (geo.check && lane < 3 * kGuardWords && LL::WAVE != LL::TAB + LL::RING) wlds[LL::guard(lane)] = kGuardPattern;
     const uint64_t t_clk0 = (ABL & kAblClock) ? __builtin_amdgcn_s_memtime() : 0;
     const uint64_t t_rt0 = (ABL & kAblClock) ? __builtin_amdgcn_s_memrealtime() : 0;
-    const uint32_t Sc = OB == 32 ? cr.words : (cr.words + 1) / 2;  // 32-bit words traced back (chunk)
 
     // per-lane LDS byte offset of this position's entry in a phase-K row (row offsets are compile-time)
     const bool upper5 = (pos >> 5) & 1;
     int aK[6];
+    constexpr int LSTR = LR ? TgTabL::REGION : 8;  // bytes between the entries of two labels
     sfor<6>([&](auto KK) {
         constexpr int K = decltype(KK)::value;
-        aK[K] = 8 * own_label(pos, K);
+        aK[K] = LSTR * own_label(pos, K);
     });
-    if constexpr (S32) aK[0] = upper5 ? 24 - aK[0] : aK[0];  // upper half: the complementary label 3 - L
+    if constexpr (S32) aK[0] = upper5 ? 3 * LSTR - aK[0] : aK[0];  // upper half: the complementary label 3 - L
     const float sg0 = upper5 ? -1.0f : 1.0f;                  // S32: sign of the phase-0 entry
     const int aU0 = aK[0] + (upper5 ? 4 : 0);  // INT phase-0 pair row: this lane's (E-, E+) half
     const int pa5 = 4 * (lane ^ 32);           // ds_bpermute address of the xor-32 partner
@@ -555,9 +644,13 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(8))
     // 0..59 of the next group a block ahead, when they are dead, measured no faster:
     // profiles/r02/ablate_twe.log.)
     const uint64_t li = (uint64_t)(lane & 31);
-    const float tagv = (float)(1 << (lane % J));
-    const float tg0 = CORE == F16 ? tagv : -tagv;  // tag of the row's own class
-    const int rowb1 = TT::row(lane), rowb2 = TT::row(64 + (int)li);
+    // LR: lane l builds the entries at table index l (stage sA) and, lanes 0..31, index 64 + l (stage sB)
+    const int sA = LR ? TgTabL::stage(lane) : lane, sB = LR ? TgTabL::stage(64 + (int)li) : 64 + (int)li;
+    const float tagv = (float)(1 << (sA % J)), tagvB = (float)(1 << (sB % J));
+    const float tg0A = CORE == F16 ? tagv : -tagv;  // tag of the row's own class (stage sA)
+    const float tg0B = CORE == F16 ? tagvB : -tagvB;
+    const int rowb1 = LR ? 0 : TT::row(lane), rowb2 = LR ? 0 : TT::row(64 + (int)li);
+    const uint32_t tabl = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)tabb;  // LDS address
 
     // V lives in [2^23, 2^24), where the fp32 ulp is 1 and the low mantissa bits ARE the low integer
     // bits: V = 1.25*2^23 + metric*2^S + 2^(S-1) + h.  The 2^(S-1) offset keeps the history field
@@ -570,27 +663,35 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(8))
     // followed by more work on their SIMD, so evening out progress buys nothing there and costs issue
     // (1.6 % per batch, profiles/r02/benchab_fair2.log).
     if constexpr (!(ABL & kAblNoFair)) fair.begin(batch + 1 < geo.nbatch ? nullptr : geo.fair, lane);
+    // fairness progress: blocks started, or in a segment launch the fraction of the segment's pass-0
+    // blocks started, scaled to 2^20 (its waves differ in length)
+    uint32_t fscale = 1u;
+    if (split) {
+        uint32_t tot = 0;
+        for (int r = 0; r < nrun; r++) tot += seg_run(sw, b0, b1, r).words + 2;
+        fscale = (1u << 20) / (tot ? tot : 1u);
+    }
     const uint64_t availB = IN::bytes(geo.availStages);
-    const uint32_t vo1 = IN::voff(lane), vo2 = IN::voff((int)li);
-    // split workgroups (uniform bookkeeping): bit q of `verified` = piece q checked exact.  vS / vE: this
-    // piece's start / end vector; vIn: the vector a re-decode starts from (left neighbour's end vector).
+    const uint32_t vo1 = IN::voff(sA), vo2 = LR ? IN::voff(sB) : IN::voff((int)li);
+    // segment workgroups (uniform bookkeeping): bit q of `verified` = segment q checked exact (segments
+    // that start at a chunk start are exact).  vS / vE: this segment's start / end vector; vIn: the vector a
+    // re-decode starts from (left neighbour's end vector).
     uint32_t verified = 1u;
+    if (split)
+        for (int q = 1; q < kWaves; q++)
+            if (seg_bound(sw, q).a == 0) verified |= 1u << q;
     float vS = 0.0f, vE = 0.0f, vIn = 0.0f;
+    uint32_t fdone = 0;  // blocks of the segment's earlier runs (fairness progress)
     for (int pass = 0;; pass++) {
     const bool runs = piece < 0 || pass == 0 || !((verified >> piece) & 1u);
     if (runs) {
-    // the words of this run: [s0, s0 + Sw) of the chunk, written from word s0 + E on; Xspec / Xcmp: the
-    // group-start blocks of the piece's left / right boundary (-1: none)
-    uint32_t s0 = 0, Sw = Sc, E = 0;
-    int Xspec = -1, Xcmp = -1;
-    if (piece >= 0) {
-        const SplitGeo sg = split_geo(Sc, piece);
-        s0 = sg.s0;
-        Sw = sg.words;
-        E = sg.E;
-        Xspec = sg.Xspec;
-        Xcmp = sg.Xcmp;
-    }
+    for (int run = 0; run < (pass == 0 ? nrun : 1); run++) {  // a re-decode pass re-runs the first run only
+    // the words of this run: [s0, s0 + Sw) of its chunk, written from word s0 + E on; Xspec / Xcmp: the
+    // group-start blocks of the segment's left / right boundary in this run (-1: none)
+    const RunGeo rg = seg_run(sw, b0, b1, run);
+    const uint32_t s0 = rg.s0, Sw = rg.words, E = rg.E;
+    const int Xspec = rg.Xspec, Xcmp = rg.Xcmp;
+    const ChunkRange cr = chunk_range(geo, sw.c0 + (uint32_t)rg.i);
     // local word k = chunk word s0 + k (32-bit words; O_B16 writes each as two 16-bit words)
     const uint64_t wOut = cr.startWord + s0;  // O_B32: output word of local word 0
     const uint64_t start = (uint64_t)cr.startWord * OB + 32ull * s0;  // first stage of the run
@@ -602,8 +703,8 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(8))
     uint32_t kb = 0;
     uint32_t tbn = pass == 0 ? kTbs - 3 * (blockIdx.x & 3) : kTbs;
     __amdgpu_buffer_rsrc_t rs = tg_rsrc<CH>(in, start + 32ull * j0, availB);
-    typename IN::raw_t rA = IN::template load<0>(rs, vo1);  // stage `lane` of the group
-    typename IN::raw_t rB = IN::template load<2>(rs, vo2);  // stage 64 + li
+    typename IN::raw_t rA = IN::template load<0>(rs, vo1);               // stage sA of the group
+    typename IN::raw_t rB = IN::template load<LR ? 0 : 2>(rs, vo2);      // stage sB
 
     // Branch-metric table reads, software-pipelined: the entries of stage r are loaded TGD stages
     // ahead; one ds_read_b64 at an even period also carries the entry of the stage 6 later.  The
@@ -711,7 +812,11 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(8))
     };
     // table row of stage phase K from the stage's (A, B) = (BM[3], BM[2]): E[L] = BM[L]*2^S + tag at
     // entries 0, 2, 4, 6 (the odd dwords are the other period's); INT phase-0 rows: the pairs (E-[L], E+[L])
-    auto put_row = [&](int rb, auto A, auto B, int K) {  // A, B: ints, or floats (IN::FAB)
+    // part 0: the entries of stage sA (all lanes), part 1: of stage sB (lanes 0..31)
+    auto put_row = [&](auto PT, auto A, auto B, int K) {  // A, B: ints, or floats (IN::FAB)
+        constexpr int part = decltype(PT)::value;
+        const int rb = part ? rowb2 : rowb1;
+        const float tg0 = part ? tg0B : tg0A;
         if constexpr (INT) {
             uint32_t* e = (uint32_t*)(tabb + rb);
             // the tag of the row's own class: -2^j (the int32 core: exchanged wins ties)
@@ -737,6 +842,10 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(8))
             asm volatile("" ::"v"(E0), "v"(E1), "v"(E2), "v"(E3));
             return;
         }
+        if constexpr (LR) {
+            lds_write_addtid4<256 * part, TgTabL::REGION>(tabl, E0, E1, E2, E3);
+            return;
+        }
         e[0] = E0;
         e[2] = E1;
         e[4] = E2;
@@ -745,26 +854,36 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(8))
     // S01: rows from the two soft values (six FMAs) instead of (A, B) = (s0 + s1, s0 - s1) (two integer
     // ops, two converts, four FMAs); fp32 cores
     constexpr bool S01 = HasS01<IN>::value && !INT;
-    auto put_row_s01 = [&](int rb, float s0, float s1) {
+    auto put_row_s01 = [&](auto PT, float s0, float s1) {
+        constexpr int part = decltype(PT)::value;
+        const int rb = part ? rowb2 : rowb1;
+        const float tg0 = part ? tg0B : tg0A;
         constexpr float SC = (float)(1 << S);
         const float X = __builtin_fmaf(s0, SC, tg0), Y = __builtin_fmaf(s0, -SC, tg0);
+        if constexpr (LR) {
+            lds_write_addtid4<256 * part, TgTabL::REGION>(tabl, __builtin_fmaf(s1, -SC, Y), __builtin_fmaf(s1, SC, Y),
+                                                          __builtin_fmaf(s1, -SC, X), __builtin_fmaf(s1, SC, X));
+            return;
+        }
         float* e = (float*)(tabb + rb);
         e[0] = __builtin_fmaf(s1, -SC, Y);
         e[2] = __builtin_fmaf(s1, SC, Y);
         e[4] = __builtin_fmaf(s1, -SC, X);
         e[6] = __builtin_fmaf(s1, SC, X);
     };
-    const int r6a = lane % 6, r6b = (int)(li + 64) % 6;
+    const int r6a = sA % 6, r6b = sB % 6;
+    using P0 = std::integral_constant<int, 0>;
+    using P1 = std::integral_constant<int, 1>;
     for (uint32_t j = j0;; j += 3) {
         // group head: the table from the inputs loaded one group ago, the next group's loads, then the
         // fairness board (its load returns during this group; nothing here waits on it)
         if constexpr (S01 && !(ABL & kAblNoTabBuild)) {
             float s0, s1;
             IN::s01(rA, s0, s1);
-            put_row_s01(rowb1, s0, s1);
+            put_row_s01(P0{}, s0, s1);
             if (lane < 32) {
                 IN::s01(rB, s0, s1);
-                put_row_s01(rowb2, s0, s1);
+                put_row_s01(P1{}, s0, s1);
             }
         } else if constexpr (!(ABL & kAblNoTabBuild)) {
             using ab_t = std::conditional_t<IN::FAB, float, int>;
@@ -773,22 +892,22 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(8))
                 else IN::ab(raw, l, A, B, geo.scale);
             };
             ab_t A, B;
-            ab(rA, lane, A, B);
-            put_row(rowb1, A, B, r6a);
+            ab(rA, sA, A, B);
+            put_row(P0{}, A, B, r6a);
             if (lane < 32) {
-                ab(rB, (int)li, A, B);
-                put_row(rowb2, A, B, r6b);
+                ab(rB, sB, A, B);
+                put_row(P1{}, A, B, r6b);
             }
         }
         if constexpr (!(ABL & kAblNoLoads)) {
             rs = tg_rsrc<CH>(in, start + 32ull * (j + 3), availB);
             rA = IN::template load<0>(rs, vo1);
-            rB = IN::template load<2>(rs, vo2);
+            rB = IN::template load<LR ? 0 : 2>(rs, vo2);
         }
         // every other group head (6 blocks): 0.7 % faster than every head, every third is 1 % slower
         // (profiles/r02/benchab_fair.log)
         if constexpr (!(ABL & kAblNoFair))
-            if ((j / 3) % 2 == 0) fair.group<6>(j, lane);
+            if ((j / 3) % 2 == 0) fair.group((fdone + j) * fscale, 3u * fscale, lane);
         if (split && pass == 0 && (int)j == Xspec) vS = V;
         if (split && (int)j == Xcmp) vE = V;
         wave_sync();
@@ -798,7 +917,9 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(8))
         if (!block(std::integral_constant<int, 4>{}, j + 2)) break;
         wave_sync();
     }
-    if (split) {  // publish the run's vectors in this wave's table LDS (dead after the run)
+    fdone += nblk - j0;
+    }  // run
+    if (split) {  // publish the segment's vectors in this wave's table LDS (dead after the run)
         wave_sync();
         float* pub = (float*)tabb;
         pub[lane] = vS;
@@ -808,7 +929,7 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(8))
     if (piece < 0) break;
     // split workgroup: evaluate the boundary checks (every wave the same), then re-decode what failed
     __syncthreads();
-    auto vec = [&](int q, int which) {  // piece q's start (0) / end (1) vector, this lane's entry
+    auto vec = [&](int q, int which) {  // segment q's start (0) / end (1) vector, this lane's entry
         return __builtin_bit_cast(uint32_t, ((const float*)(lds + q * LL::WAVE + LL::TAB_OFF))[64 * which + lane]);
     };
     for (int q = 1; q < kWaves; q++)

@@ -42,10 +42,10 @@ struct Geom {
     uint32_t nchunks;
     uint32_t* fair;        // per-SIMD progress board (kFairBoardWords, empty at rest) or null
     float scale;           // LLR input (channel ids 8 + base): SoftDecisionPacker scale, else unused
-    // split launch (vd_kernel_tg.h "split chunks"): chunks >= nwhole are decoded as kWaves pieces, one
-    // workgroup each (their boundary vectors stay in the workgroup's LDS); 0 = every chunk whole
-    uint32_t nwhole = 0;
-    uint32_t* stats = nullptr;   // count of split pieces re-decoded (or null)
+    // segment launch (vd_kernel_tg.h "segment launches"): workgroup g decodes chunks [seg[g], seg[g+1]) as
+    // kWaves segments (their boundary vectors stay in the workgroup's LDS); null = one chunk per wave
+    const uint32_t* seg = nullptr;
+    uint32_t* stats = nullptr;   // count of segments re-decoded (or null)
     // LDS guard check (tests): non-null = write guard words around every wave's table and ring and count
     // the ones found overwritten at kernel exit into *check
     uint32_t* check = nullptr;
@@ -125,15 +125,18 @@ __device__ __forceinline__ uint32_t simd_slot()
 
 // Fairness controller.  The SIMD arbiter favours the oldest wave, so left alone the waves sharing a
 // SIMD finish up to 2x apart and the tail of the launch runs at low occupancy (tools/vd_ablate clock
-// stamps).  At every other 3-block group head each wave posts the blocks it has started to its own board
-// word and sets its issue priority from its lag behind the mean of the SIMD's waves, read at the
-// previous call.  Posting is a plain store and reading one 64-byte load (16 lanes): both stay in the XCD's L2
-// (all waves of a SIMD are on one XCD), so the board adds no HBM or fabric traffic -- a returning atomic
-// per group went past the L2 and cost 11 MB of writes per launch (profiles/r02).
+// stamps).  At every other 3-block group head each wave posts its progress to its own board word and sets
+// its issue priority from its lag behind the mean of the SIMD's waves, read at the previous call.
+// Progress is in blocks started, or, when the waves of a launch differ in length (segment launches,
+// vd_kernel_tg.h), the fraction started scaled to 2^20, so that waves of unequal work end together.
+// Posting is a plain store and reading one 64-byte load (16 lanes): both stay in the XCD's L2 (all
+// waves of a SIMD are on one XCD), so the board adds no HBM or fabric traffic -- a returning atomic per
+// group went past the L2 and cost 11 MB of writes per launch (profiles/r02).
 struct Fair {
     uint32_t* mine = nullptr;   // this wave's word
     uint32_t* simd = nullptr;   // the SIMD's kFairWaves words
     uint32_t seen = kFairEmpty; // lane l < kFairWaves: word l as read at the previous group head
+    uint32_t last = kFairEmpty; // this wave's value posted at the previous call
 
     __device__ __forceinline__ void begin(uint32_t* board, int lane)
     {
@@ -143,12 +146,12 @@ struct Fair {
         mine = simd + wid;
         if (lane == 0) __hip_atomic_store(mine, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
     }
-    // group head; j = blocks started so far (a multiple of 3); PREV = blocks since the previous call
-    template <int PREV = 3>
-    __device__ __forceinline__ void group(uint32_t j, int lane)
+    // group head: now = progress so far, unit3 = the progress of 3 blocks (the priority step); both in the
+    // same units for all waves of the launch (uniform values)
+    __device__ __forceinline__ void group(uint32_t now, uint32_t unit3, int lane)
     {
         if (!mine) return;
-        if (j > 0) {
+        if (last != kFairEmpty) {
             const bool act = lane < kFairWaves && seen != kFairEmpty;
             const uint32_t n = (uint32_t)__builtin_popcountll(__ballot(act));
             uint32_t x = act ? seen : 0u;
@@ -158,15 +161,16 @@ struct Fair {
             x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xF, 0xF, true);
             x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xF, 0xF, true);
             const uint32_t sum = (uint32_t)__builtin_amdgcn_readlane((int)x, 15);
-            // (own - mean) * n in blocks; own word read back as posted at the previous call (j - PREV).
-            // 32-bit scalar arithmetic (n <= 16, j < 2^26): 64-bit compares would run on the VALU.
-            const int32_t d = (int32_t)(j - PREV) * (int32_t)n - (int32_t)sum, n3 = 3 * (int32_t)n;
+            // (own - mean) * n; own = the value posted at the previous call, which the read saw.  32-bit
+            // scalar arithmetic (n <= 16, values < 2^26): 64-bit compares would run on the VALU.
+            const int32_t d = (int32_t)last * (int32_t)n - (int32_t)sum, n3 = (int32_t)unit3 * (int32_t)n;
             if (d <= -n3) __builtin_amdgcn_s_setprio(3);
             else if (d <= 0) __builtin_amdgcn_s_setprio(2);
             else if (d <= n3) __builtin_amdgcn_s_setprio(1);
             else __builtin_amdgcn_s_setprio(0);
         }
-        if (lane == 0) __hip_atomic_store(mine, j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+        if (lane == 0) __hip_atomic_store(mine, now, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+        last = now;
         const uint32_t* w = simd + (lane & (kFairWaves - 1));
         seen = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }

@@ -32,7 +32,7 @@ VCC_WRITERS = re.compile(r"\bv_(cmp_\w+_e32|cmp_class_\w+_e32|add_co_u32\w*|sub_
                          r"addc_co_u32\w*|subb_co_u32\w*|subbrev_co_u32\w*|div_scale\w*)\b|\bvcc\b")
 EXEC_WRITERS = re.compile(r"\b(v_cmpx_\w+|s_\w+_saveexec_b\d+|s_\w+_wrexec_b\d+)\b|\bexec\b")
 M0_WRITERS = re.compile(r"\bm0\b")
-PHYS_VGPR = re.compile(r"\bv(\d+)\b|\bv\[(\d+):(\d+)\]")
+PHYS_VGPR = re.compile(r"(?<!\[)\bv(\d+)\b|\bv\[(\d+):(\d+)\]")  # not a named operand %[v0]
 
 
 def _macros(text):
@@ -54,10 +54,16 @@ def _asm_statements(text):
 
 
 def _split(stmt):
-    """(template strings, constraint/clobber part) of an asm statement"""
+    """(template strings, constraint/clobber part) of an asm statement: split at the first ':' outside the
+    string literals (templates contain ':' themselves, e.g. offset:%[o])"""
     body = stmt[stmt.index("(") + 1:-1]
-    parts = body.split(":", 1)
-    return parts[0], (parts[1] if len(parts) > 1 else "")
+    inq = False
+    for i, ch in enumerate(body):
+        if ch == '"' and (i == 0 or body[i - 1] != "\\"):
+            inq = not inq
+        elif ch == ":" and not inq:
+            return body[:i], body[i + 1:]
+    return body, ""
 
 
 def _statements():
@@ -83,10 +89,25 @@ def test_scc_writing_asm_declares_scc():
     assert not bad, "asm writing SCC without a \"scc\" clobber: " + ", ".join(bad)
 
 
+def _saves_m0(tmpl):
+    """M0 is reserved: the compiler ignores an "m0" clobber, so a statement that writes M0 must save it first
+    and restore it last (s_mov_b32 %[t], m0 ... s_mov_b32 m0, %[t])"""
+    ins = [i.strip() for i in re.split(r"\s{2,}|\n|\\n", tmpl.replace('"', " ")) if i.strip()]
+    m = re.match(r"s_mov_b32 (%\[\w+\]), m0$", ins[0]) if ins else None
+    return bool(m) and ins[-1] == f"s_mov_b32 m0, {m.group(1)}"
+
+
 @pytest.mark.parametrize("reg,pat", [("vcc", VCC_WRITERS), ("exec", EXEC_WRITERS), ("m0", M0_WRITERS)])
 def test_vcc_exec_m0_writing_asm_declares_them(reg, pat):
-    bad = [w for w, stmt, tmpl, rest in _statements() if pat.search(tmpl) and f'"{reg}"' not in rest]
+    bad = [w for w, stmt, tmpl, rest in _statements() if pat.search(tmpl) and f'"{reg}"' not in rest
+           and not (reg == "m0" and _saves_m0(tmpl))]
     assert not bad, f"asm writing {reg} without a \"{reg}\" clobber: " + ", ".join(bad)
+
+
+def test_m0_save_restore_rule_is_not_vacuous():
+    hits = [w for w, stmt, tmpl, rest in _statements() if M0_WRITERS.search(tmpl)]
+    assert hits and all(_saves_m0(t) for w, s, t, r in _statements() if M0_WRITERS.search(t))
+    assert not _saves_m0("s_mov_b32 m0, %[b]  ds_write_addtid_b32 %[v]")
 
 
 def test_physical_vgprs_are_declared():

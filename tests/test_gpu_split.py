@@ -1,7 +1,8 @@
-"""Split launches (vd_kernel_tg.h "split chunks"): with 6400 chunks on 1024 SIMDs the
-last 256 chunks are decoded as 4 pieces each, pieces 1-3 from a speculative start that is checked at
-the piece boundary after a workgroup barrier; a piece whose check fails re-decodes from its left
-neighbour's end vector.  The decoded words must be identical to the unsplit launch (VD_NO_SPLIT=1) and
+"""Segment launches (vd_kernel_tg.h "segment launches"): single 6400-chunk launches cut
+into workgroup segments ("pieces": the last 256 chunks in 4 pieces each; "thirds": workgroups of 3 or 4
+chunks in 4 segments that cross chunk boundaries).  A segment that starts inside a chunk starts
+speculatively and is checked at its boundary after a workgroup barrier; one whose check fails
+re-decodes from its left neighbour's end vector.  The decoded words must be identical to the unsplit launch (VD_NO_SPLIT=1) and
 to the oracle, at SNRs where the speculation always converges and where it often does not (SNR 0: the
 re-decode passes run, and the test requires that they did)."""
 import os
@@ -13,9 +14,14 @@ from vitdec import FP32, HARD, M_B16, M_B32, M_FP16, O_B16, SOFT4, SOFT8, SOFT16
 from test_gpu_parity import gpu_decode, name
 
 
-def decode_split_and_whole(gpu, opt, packed, n):
+def decode_split_and_whole(gpu, opt, packed, n, mode=None):
     before = gpu.split_redecodes()
-    out = gpu_decode(gpu, opt, packed)
+    if mode:
+        os.environ["VD_SPLIT"] = mode
+    try:
+        out = gpu_decode(gpu, opt, packed)
+    finally:
+        os.environ.pop("VD_SPLIT", None)
     redecodes = gpu.split_redecodes() - before
     os.environ["VD_NO_SPLIT"] = "1"
     try:
@@ -29,12 +35,14 @@ def decode_split_and_whole(gpu, opt, packed, n):
 @pytest.mark.parametrize("opt", [HARD | M_B32, SOFT8 | M_B16, SOFT4 | M_B32, FP32 | M_FP16, SOFT16 | M_B32,
                                  HARD | M_B32 | O_B16, SOFT8 | M_B16 | O_B16, FP32 | M_FP16 | O_B16], ids=name)
 @pytest.mark.parametrize("snr", [0.0, 1.0, 3.0])
-def test_split_equals_whole_16m(gpu, vo, opt, snr):
-    # 78 32-bit words per chunk: split (>= 64); O_B16: 156-157 16-bit words per chunk (odd counts: the
-    # last piece writes the chunk's final half word only)
+@pytest.mark.parametrize("mode", ["pieces", "thirds"])
+def test_split_equals_whole_16m(gpu, vo, opt, snr, mode):
+    # 78 32-bit words per chunk: segment launch (>= 64); O_B16: 156-157 16-bit words per chunk (odd
+    # counts: the last segment of a chunk writes its final half word only).  pieces: 256 chunks in 4
+    # pieces; thirds: workgroups of 3 (4) chunks in 4 segments, segments crossing chunk boundaries
     n = 16_000_000
     bits, packed = gpu_sim(gpu, opt, n, snr)
-    out, whole, redecodes = decode_split_and_whole(gpu, opt, packed, n)
+    out, whole, redecodes = decode_split_and_whole(gpu, opt, packed, n, mode)
     bad = np.flatnonzero(out != whole)
     assert bad.size == 0, f"{bad.size} words differ (re-decoded pieces: {redecodes}), first {bad[:5]}"
     ref, ok = vo.decode(opt, packed, nthreads=16)
@@ -60,15 +68,20 @@ def gpu_sim(gpu, opt, n, snr):
 @pytest.mark.slow
 @pytest.mark.parametrize("snr", [0.0, 1.2])
 @pytest.mark.parametrize("opt", [HARD | M_B32, SOFT8 | M_B16], ids=name)
-def test_split_full_32m_matches_oracle(gpu, vo, opt, snr):
+@pytest.mark.parametrize("mode", ["pieces", "thirds"])
+def test_split_full_32m_matches_oracle(gpu, vo, opt, snr, mode):
     bits, packed = gpu_sim(gpu, opt, 32_000_000, snr)
     before = gpu.split_redecodes()
-    out = gpu_decode(gpu, opt, packed)
+    os.environ["VD_SPLIT"] = mode
+    try:
+        out = gpu_decode(gpu, opt, packed)
+    finally:
+        os.environ.pop("VD_SPLIT", None)
     redecodes = gpu.split_redecodes() - before
     ref, ok = vo.decode(opt, packed, nthreads=16)
     assert ok
     np.testing.assert_array_equal(out, ref)
-    print(f"snr {snr}: {redecodes} pieces of the 256 split chunks re-decoded")
+    print(f"snr {snr}, {mode}: {redecodes} segments re-decoded")
     if snr == 0.0:
         assert redecodes > 0
 

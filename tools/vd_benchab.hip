@@ -13,6 +13,7 @@
 #include <vector>
 #include <algorithm>
 #include "../gpu-accelerated-viterbi-decoder_amd/csrc/vd_kernel_tg.h"
+#include "../gpu-accelerated-viterbi-decoder_amd/csrc/vd_segplan.h"
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP error %s at %d\n", hipGetErrorString(e), __LINE__); exit(1); } } while (0)
 using KFn = void (*)(const void*, void*, vd::Geom);
 
@@ -68,11 +69,19 @@ int main(int argc, char** argv)
     uint32_t* stats;
     CK(hipMalloc(&stats, 4));
     CK(hipMemset(stats, 0, 4));
-    g.nwhole = 6144; g.stats = stats;
+    {   // single launches: the product's segment table (round 2's pieces)
+        int cus = 0;
+        CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
+        const std::vector<uint32_t> t = vd::seg_table(4 * cus, false);
+        uint32_t* tb; CK(hipMalloc(&tb, t.size() * 4));
+        CK(hipMemcpy(tb, t.data(), t.size() * 4, hipMemcpyHostToDevice));
+        g.seg = tb;
+    }
+    g.stats = stats;
     const Variant vs[] = {
         {"product (xor-32 by ds_bpermute)", (KFn)vd::vd_decode_tg<vd::HARD, vd::B32, 32, 0>, (KFn)vd::vd_decode_tg<vd::SOFT8, vd::B16, 32, 0>},
         {"no fairness controller (ABL 256)", (KFn)vd::vd_decode_tg<vd::HARD, vd::B32, 32, 256>, (KFn)vd::vd_decode_tg<vd::SOFT8, vd::B16, 32, 256>},
-        {"no LDS guard space (19,968 B per workgroup)", (KFn)vd::vd_decode_tg<vd::HARD, vd::B32, 32, vd::kAblNoGuardSpace>, (KFn)vd::vd_decode_tg<vd::SOFT8, vd::B16, 32, vd::kAblNoGuardSpace>},
+        {"interleaved-row table, ds_write2_b32 (round 2)", (KFn)vd::vd_decode_tg<vd::HARD, vd::B32, 32, vd::kAblRowTable>, (KFn)vd::vd_decode_tg<vd::SOFT8, vd::B16, 32, vd::kAblRowTable>},
     };
     const int nv = sizeof(vs) / sizeof(vs[0]);
     // bench conditions (bench.py): each workload's `steps` batches as one batched launch, every batch its
@@ -89,7 +98,7 @@ int main(int argc, char** argv)
         CK(hipMemcpy((char*)bS + k * strS, inS, hs.size() * 4, hipMemcpyDeviceToDevice));
     }
     vd::Geom gh = g, gs = g;
-    gh.nwhole = gs.nwhole = 0;
+    gh.seg = gs.seg = nullptr;
     gh.nbatch = gs.nbatch = (uint32_t)steps;
     gh.inStride = strH; gs.inStride = strS; gh.outStride = gs.outStride = ostr;
     const unsigned gridB = 1600u * (unsigned)steps;
@@ -166,7 +175,7 @@ int main(int argc, char** argv)
         hipEvent_t e0, e1, e2;
         CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1)); CK(hipEventCreate(&e2));
         vd::Geom gb = g;
-        gb.nwhole = 0; gb.nbatch = (uint32_t)steps;
+        gb.seg = nullptr; gb.nbatch = (uint32_t)steps;
         const unsigned gridb = 1600u * (unsigned)steps;
         std::vector<float> th1, ts1, thb, tsb;
         for (int r = 0; r < groups + 1; r++) {

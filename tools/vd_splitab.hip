@@ -1,6 +1,7 @@
-// vd_splitab.hip -- timing-only A/B of the split launch (vd_kernel_tg.h "split chunks") against the
-// plain launch, interleaved, plus per-wave clock stamps (ABL 32) of both: waves per SIMD and when
-// each SIMD's last wave ends.
+// vd_splitab.hip -- timing-only A/B of single launches (the reference run()'s unit of work, one 32M-bit
+// batch per launch): plain (one chunk per wave), "pieces" and "thirds" segment launches (vd_kernel_tg.h
+// "segment launches", tables from vd_segplan.h), isolated and back to back, with per-wave clock stamps
+// (kAblClock): waves per SIMD, SIMD and XCD end times, clocks.  The modes' decoded words are compared.
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstdlib>
@@ -8,6 +9,7 @@
 #include <map>
 #include <algorithm>
 #include "../gpu-accelerated-viterbi-decoder_amd/csrc/vd_kernel_tg.h"
+#include "../gpu-accelerated-viterbi-decoder_amd/csrc/vd_segplan.h"
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP error %s at %d\n", hipGetErrorString(e), __LINE__); exit(1); } } while (0)
 using KFn = void (*)(const void*, void*, vd::Geom);
 int main(int argc, char** argv)
@@ -15,7 +17,7 @@ int main(int argc, char** argv)
     const size_t N = 32000000, inBytes = 2 * N / 8;  // HARD
     void *in, *out;
     CK(hipMalloc(&in, inBytes));
-    CK(hipMalloc(&out, (16u << 20) + 7168 * 48));
+    CK(hipMalloc(&out, (16u << 20) + 8192 * 48));
     // a K=7 (0171, 0133) codeword through a binary symmetric channel (flip probability argv[2], default
     // 0.04, about what 2 dB gives hard decisions), HARD format: stage t -> bits 31-2(t%16), 30-2(t%16)
     std::vector<uint32_t> h(inBytes / 4, 0u);
@@ -31,6 +33,8 @@ int main(int argc, char** argv)
         h[t / 16] |= (o0 << (31 - 2 * (t % 16))) | (o1 << (30 - 2 * (t % 16)));
     }
     CK(hipMemcpy(in, h.data(), inBytes, hipMemcpyHostToDevice));
+    int cus = 0;
+    CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
     vd::Geom g;
     g.packNum = (N - 64) / 32;
     g.nchunks = 6400;
@@ -41,40 +45,59 @@ int main(int argc, char** argv)
     uint32_t* stats;
     CK(hipMalloc(&stats, 4));
     CK(hipMemset(stats, 0, 4));
-    auto launch = [&](KFn f, bool split) {
+    // mode 0: plain; 1: pieces; 2: thirds
+    const char* names[3] = {"plain", "pieces", "thirds"};
+    uint32_t* tab[3] = {nullptr, nullptr, nullptr};
+    unsigned grid[3] = {1600, 0, 0};
+    for (int m = 1; m < 3; m++) {
+        std::vector<uint32_t> t = vd::seg_table(4 * cus, m == 2);
+        if (t.empty()) { printf("no %s table for %d CUs\n", names[m], cus); return 1; }
+        CK(hipMalloc(&tab[m], t.size() * 4));
+        CK(hipMemcpy(tab[m], t.data(), t.size() * 4, hipMemcpyHostToDevice));
+        grid[m] = (unsigned)(t.size() - 1);
+    }
+    auto launch = [&](KFn f, int m) {
         vd::Geom q = g;
-        if (split) { q.nwhole = 6144; q.stats = stats; }
-        hipLaunchKernelGGL(f, dim3(split ? 1792 : 1600), dim3(256), 0, 0, in, out, q);
+        if (m) { q.seg = tab[m]; q.stats = stats; }
+        hipLaunchKernelGGL(f, dim3(grid[m]), dim3(256), 0, 0, in, out, q);
     };
-    KFn f0 = (KFn)vd::vd_decode_tg<vd::HARD, vd::B32, 32, 0>, f32 = (KFn)vd::vd_decode_tg<vd::HARD, vd::B32, 32, 32>;
+    KFn f0 = (KFn)vd::vd_decode_tg<vd::HARD, vd::B32, 32, 0>, fc = (KFn)vd::vd_decode_tg<vd::HARD, vd::B32, 32, vd::kAblClock>;
+    // the modes decode the same words
+    {
+        std::vector<uint32_t> a(g.packNum), b(g.packNum);
+        for (int m = 0; m < 3; m++) {
+            CK(hipMemset(out, 0, g.packNum * 4));
+            launch(f0, m);
+            CK(hipMemcpy(m ? b.data() : a.data(), out, g.packNum * 4, hipMemcpyDeviceToHost));
+            if (m) {
+                size_t bad = 0;
+                for (size_t k = 0; k < a.size(); k++) bad += a[k] != b[k];
+                printf("exact twin %s vs plain: %zu of %zu words differ\n", names[m], bad, a.size());
+            }
+        }
+    }
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
     const int rounds = argc > 1 ? atoi(argv[1]) : 10;
-    std::vector<float> t[2];
+    std::vector<float> t[3], tb[3];
     for (int r = 0; r < rounds + 2; r++)
-        for (int s = 0; s < 2; s++) {
-            CK(hipEventRecord(e0)); launch(f0, s); CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
-            float ms; CK(hipEventElapsedTime(&ms, e0, e1)); if (r >= 2) t[s].push_back(ms);
+        for (int m = 0; m < 3; m++) {
+            CK(hipEventRecord(e0)); launch(f0, m); CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
+            float ms; CK(hipEventElapsedTime(&ms, e0, e1)); if (r >= 2) t[m].push_back(ms);
+            // back to back (as a caller streams batches): 20 launches between two events
+            CK(hipEventRecord(e0)); for (int k = 0; k < 20; k++) launch(f0, m); CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
+            CK(hipEventElapsedTime(&ms, e0, e1)); if (r >= 2) tb[m].push_back(ms / 20);
         }
-    for (int s = 0; s < 2; s++) { std::sort(t[s].begin(), t[s].end());
-        printf("%-8s median %.4f ms  min %.4f ms\n", s ? "split" : "plain", t[s][t[s].size() / 2], t[s][0]); }
-    // back to back (the reference run()'s unit of work, one launch per batch, as a caller streams batches):
-    // per launch wall time between events around 20 launches, against the kernel span the clock stamps of
-    // single launches show below; the difference is the launch-to-launch gap
-    for (int s = 0; s < 2; s++) {
-        std::vector<float> tb;
-        for (int r = 0; r < rounds; r++) {
-            CK(hipEventRecord(e0)); for (int k = 0; k < 20; k++) launch(f0, s); CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
-            float ms; CK(hipEventElapsedTime(&ms, e0, e1)); tb.push_back(ms / 20);
-        }
-        std::sort(tb.begin(), tb.end());
-        printf("%-8s back to back (20 launches): median %.4f ms per launch\n", s ? "split" : "plain", tb[tb.size() / 2]);
+    for (int m = 0; m < 3; m++) {
+        std::sort(t[m].begin(), t[m].end()); std::sort(tb[m].begin(), tb[m].end());
+        printf("%-7s isolated median %.4f ms  back to back (20) median %.4f ms per launch -> %.1f Gb/s\n", names[m],
+               t[m][t[m].size() / 2], tb[m][tb[m].size() / 2], (double)(N - 64) / (tb[m][tb[m].size() / 2] * 1e-3) / 1e9);
     }
     uint32_t redec = 0; CK(hipMemcpy(&redec, stats, 4, hipMemcpyDeviceToHost));
-    printf("re-decoded split chunks over all split launches: %u\n", redec);
-    for (int s = 0; s < 2; s++) {
-        const int nw = s ? 7168 : 6400;
-        for (int r = 0; r < 3; r++) launch(f32, s);
+    printf("re-decoded segments over all segment launches: %u\n", redec);
+    for (int m = 0; m < 3; m++) {
+        const int nw = (int)grid[m] * 4;
+        for (int r = 0; r < 3; r++) launch(fc, m);
         CK(hipDeviceSynchronize());
         std::vector<uint64_t> d(nw * 6);
         CK(hipMemcpy(d.data(), (char*)out + (16u << 20), d.size() * 8, hipMemcpyDeviceToHost));
@@ -83,43 +106,34 @@ int main(int argc, char** argv)
         std::map<uint32_t, std::vector<int>> bysimd;
         for (int w = 0; w < nw; w++) {
             uint32_t hw = (uint32_t)d[6 * w + 4], xc = (uint32_t)d[6 * w + 5] & 7;
-            uint32_t key = (xc << 16) | (hw & 0xFFF0);
-            bysimd[key].push_back(w);
+            bysimd[(xc << 16) | (hw & 0xFFF0)].push_back(w);
         }
-        std::map<int, int> hist; std::vector<double> simdEnd; std::map<int, std::vector<double>> endByCount;
-        int piecesPerSimdMax = 0; std::map<int, int> pieceHist;
+        std::map<int, int> hist; std::vector<double> simdEnd;
         for (auto& kv : bysimd) {
             hist[(int)kv.second.size()]++;
-            double e = 0; int pc = 0;
-            for (int w : kv.second) { e = std::max(e, (d[6 * w + 3] - r0) / 100.0); if (s && w >= 6144) pc++; }
-            simdEnd.push_back(e); endByCount[(int)kv.second.size()].push_back(e);
-            pieceHist[pc]++; piecesPerSimdMax = std::max(piecesPerSimdMax, pc);
+            double e = 0;
+            for (int w : kv.second) e = std::max(e, (d[6 * w + 3] - r0) / 100.0);
+            simdEnd.push_back(e);
         }
         std::sort(simdEnd.begin(), simdEnd.end());
-        printf("=== %s: span %.1f us, SIMDs %zu, waves/SIMD:", s ? "split" : "plain", (r1 - r0) / 100.0, bysimd.size());
+        printf("=== %s: span %.1f us, SIMDs %zu, waves/SIMD:", names[m], (r1 - r0) / 100.0, bysimd.size());
         for (auto& kv : hist) printf(" %d:%d", kv.first, kv.second);
         printf("\n    SIMD end us: min %.1f p10 %.1f med %.1f p90 %.1f max %.1f\n", simdEnd[0], simdEnd[simdEnd.size() / 10],
                simdEnd[simdEnd.size() / 2], simdEnd[simdEnd.size() * 9 / 10], simdEnd.back());
-        for (auto& kv : endByCount) { auto v = kv.second; std::sort(v.begin(), v.end());
-            printf("    SIMDs with %d waves: %zu, end med %.1f max %.1f\n", kv.first, v.size(), v[v.size() / 2], v.back()); }
-        {   // start skew and clock: wave start times, per-XCD median end and clock (s_memtime / s_memrealtime)
-            std::vector<double> st; std::map<uint32_t, std::vector<double>> xend, xmhz;
-            for (int w = 0; w < nw; w++) {
-                if (d[6 * w + 2] == 0) continue;
-                st.push_back((d[6 * w + 2] - r0) / 100.0);
-                const uint32_t xc = (uint32_t)d[6 * w + 5] & 7;
-                xend[xc].push_back((d[6 * w + 3] - r0) / 100.0);
-                xmhz[xc].push_back((double)(d[6 * w + 1] - d[6 * w]) / (double)(d[6 * w + 3] - d[6 * w + 2]) * 100.0);
-            }
-            std::sort(st.begin(), st.end());
-            printf("    wave start us: min %.1f p10 %.1f med %.1f p90 %.1f max %.1f\n", st[0], st[st.size() / 10], st[st.size() / 2],
-                   st[st.size() * 9 / 10], st.back());
-            for (auto& kv : xend) { auto a = kv.second, b = xmhz[kv.first]; std::sort(a.begin(), a.end()); std::sort(b.begin(), b.end());
-                printf("    XCD %u: wave end med %.1f max %.1f, clock med %.0f MHz\n", kv.first, a[a.size() / 2], a.back(), b[b.size() / 2]); }
+        std::vector<double> st, we; std::map<uint32_t, std::vector<double>> xend, xmhz;
+        for (int w = 0; w < nw; w++) {
+            if (d[6 * w + 2] == 0) continue;
+            st.push_back((d[6 * w + 2] - r0) / 100.0);
+            we.push_back((d[6 * w + 3] - r0) / 100.0);
+            const uint32_t xc = (uint32_t)d[6 * w + 5] & 7;
+            xend[xc].push_back((d[6 * w + 3] - r0) / 100.0);
+            xmhz[xc].push_back((double)(d[6 * w + 1] - d[6 * w]) / (double)(d[6 * w + 3] - d[6 * w + 2]) * 100.0);
         }
-        if (s) { printf("    piece waves per SIMD:"); for (auto& kv : pieceHist) printf(" %d:%d", kv.first, kv.second); printf("\n");
-            std::vector<double> pe; for (int w = 6144; w < nw; w++) pe.push_back((d[6 * w + 3] - r0) / 100.0);
-            std::sort(pe.begin(), pe.end()); printf("    piece wave end us: min %.1f med %.1f max %.1f\n", pe[0], pe[pe.size() / 2], pe.back()); }
+        std::sort(st.begin(), st.end()); std::sort(we.begin(), we.end());
+        printf("    wave start us: min %.1f med %.1f max %.1f; wave end us: min %.1f p10 %.1f med %.1f max %.1f\n", st[0],
+               st[st.size() / 2], st.back(), we[0], we[we.size() / 10], we[we.size() / 2], we.back());
+        for (auto& kv : xend) { auto a = kv.second, b = xmhz[kv.first]; std::sort(a.begin(), a.end()); std::sort(b.begin(), b.end());
+            printf("    XCD %u: wave end med %.1f max %.1f, clock med %.0f MHz\n", kv.first, a[a.size() / 2], a.back(), b[b.size() / 2]); }
     }
     return 0;
 }
