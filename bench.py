@@ -32,7 +32,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md)
 SNR_DB = 2.0
 WARM_S = 0.5      # minimum warm-up (seconds of steps) before the timed region
 POOL = 128        # at most this many resident batches per workload (128 SOFT8 batches: 8.2 GB of input)
-PMC_ROUND = "r02"  # profiles/<round>/pmc_summary.json, profiles/<round>/ablate_batched.log
+PMC_ROUND = "r03"  # profiles/<round>/pmc_summary.json, profiles/<round>/ablate_batched.log
 
 WORKLOADS = [
     ("hard_b32", vitdec.HARD | vitdec.M_B32 | vitdec.O_B32),
@@ -681,12 +681,13 @@ def main():
                 sums0.append(x)
         bers.append(max(ber_k))
         sums.append(ck)
+    # side measurements, the kernel-only ones first (the PCIe one leaves the GPU waiting on host copies)
     side = rank == 0 and metric_run
-    llr = None if (args.no_llr or not side) else llr_side_measurement(dev, sptr, stream)
-    pcie = None if (args.no_pcie or not side) else pcie_side_measurement(batches, dev)
-    chan = None if (args.no_channel or not side) else channel_side_measurement(dev, sptr)
     other = None if (args.no_other or not side) else other_configs_side_measurement(dev, sptr, stream)
     single = None if (args.no_other or not side) else single_launch_side_measurement(batches, stream, sptr)
+    llr = None if (args.no_llr or not side) else llr_side_measurement(dev, sptr, stream)
+    chan = None if (args.no_channel or not side) else channel_side_measurement(dev, sptr)
+    pcie = None if (args.no_pcie or not side) else pcie_side_measurement(batches, dev)
     # the same collectives at every N (N = 1: a 1-rank RCCL group)
     elapsed = max_over_ranks(elapsed, dev)
     gathered = gather_checksums(sums + sums0, dev, world)

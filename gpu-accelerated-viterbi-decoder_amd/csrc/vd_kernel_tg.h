@@ -519,8 +519,8 @@ struct SegWG {
     uint32_t c0;
     int k;
     uint32_t W0, W1, W2, W3;
-    __device__ __forceinline__ uint32_t W(int i) const { return i == 0 ? W0 : i == 1 ? W1 : i == 2 ? W2 : W3; }
-    __device__ __forceinline__ uint32_t cum(int i) const  // words of chunks 0 .. i-1
+    __host__ __device__ __forceinline__ uint32_t W(int i) const { return i == 0 ? W0 : i == 1 ? W1 : i == 2 ? W2 : W3; }
+    __host__ __device__ __forceinline__ uint32_t cum(int i) const  // words of chunks 0 .. i-1
     {
         return (i > 0 ? W0 : 0u) + (i > 1 ? W1 : 0u) + (i > 2 ? W2 : 0u) + (i > 3 ? W3 : 0u);
     }
@@ -530,7 +530,7 @@ struct SegPos {
     uint32_t a;  // local word; a > 0: (a + 1) % 3 == 0 and a >= kSplitWarm
 };
 // boundary q (0 .. kWaves) of the workgroup's segments
-__device__ __forceinline__ SegPos seg_bound(const SegWG& w, int q)
+__host__ __device__ __forceinline__ SegPos seg_bound(const SegWG& w, int q)
 {
     if (q == 0) return {0, 0u};
     if (q == kWaves) return {w.k, 0u};
@@ -549,7 +549,7 @@ struct RunGeo {
     uint32_t s0, words, E;
     int Xspec, Xcmp;
 };
-__device__ __forceinline__ RunGeo seg_run(const SegWG& w, SegPos b0, SegPos b1, int r)
+__host__ __device__ __forceinline__ RunGeo seg_run(const SegWG& w, SegPos b0, SegPos b1, int r)
 {
     RunGeo g;
     g.i = b0.i + r;
@@ -562,7 +562,7 @@ __device__ __forceinline__ RunGeo seg_run(const SegWG& w, SegPos b0, SegPos b1, 
     g.Xcmp = b == W ? -1 : (int)(b + 1 - g.s0);
     return g;
 }
-__device__ __forceinline__ int seg_nruns(SegPos b0, SegPos b1) { return b1.i - b0.i + (b1.a != 0 ? 1 : 0); }
+__host__ __device__ __forceinline__ int seg_nruns(SegPos b0, SegPos b1) { return b1.i - b0.i + (b1.a != 0 ? 1 : 0); }
 
 // ================================================================ the kernel: one chunk per wave
 template <int CH, int CORE, int OB, int ABL = 0>
