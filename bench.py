@@ -683,9 +683,12 @@ def main():
         sums.append(ck)
     # side measurements, the kernel-only ones first (the PCIe one leaves the GPU waiting on host copies)
     side = rank == 0 and metric_run
-    other = None if (args.no_other or not side) else other_configs_side_measurement(dev, sptr, stream)
+    # the other formats and the fused float input run in launches of as many batches as the timed region's
+    # (at least 20): a shorter launch carries more of the once-per-launch ramp and tail per batch
+    side_reps = max(20, P)
+    other = None if (args.no_other or not side) else other_configs_side_measurement(dev, sptr, stream, side_reps)
     single = None if (args.no_other or not side) else single_launch_side_measurement(batches, stream, sptr)
-    llr = None if (args.no_llr or not side) else llr_side_measurement(dev, sptr, stream)
+    llr = None if (args.no_llr or not side) else llr_side_measurement(dev, sptr, stream, side_reps)
     chan = None if (args.no_channel or not side) else channel_side_measurement(dev, sptr)
     pcie = None if (args.no_pcie or not side) else pcie_side_measurement(batches, dev)
     # the same collectives at every N (N = 1: a 1-rank RCCL group)

@@ -67,7 +67,8 @@ struct TgFmt {
 // fits, so |V +- E| < 2^31.  The CLI default SNR 15 (saturated soft values on the codeword: the best
 // path gains BMmax every stage) is in the parity tests; tests/test_metric_range.py checks the bounds.
 
-// Interleaved-row table (SOFT16; the fp32 cores use TgTabL below): per 96-stage group, 16 periods of 6 rows (row K = stage phase); a row holds
+// Interleaved-row table (round 2's layout, now the kAblRowTable A/B variant; the product uses TgTabL below):
+// per 96-stage group, 16 periods of 6 rows (row K = stage phase); a row holds
 // E[L] = BM[L]*2^S + tag for the four labels L.  Rows K of periods 2m and 2m+1 are interleaved entry by
 // entry, so a lane's entries for stages t and t+6 are one 8-byte ds_read_b64: entry e of row r sits at
 // row(r) + 8e.  The SOFT16 (INT, M_B32) phase-0 rows hold, per label, the pair (E-, E+) of both tag
@@ -97,16 +98,29 @@ struct TgTab {
 // scattered row addresses).  Against the interleaved-row table (TgTab, kAblRowTable): HARD 0.1627 ->
 // 0.1582 ms, SOFT8 0.1655 -> 0.1632 ms per batch under bench conditions, exact twins
 // (profiles/r03/benchab_label_regions.log).
-struct TgTabL {
-    static constexpr int REGION = 104 * 4;  // bytes per label region
+// ALT (SOFT16, int32 patterns): the M_B32 upper position half needs the other tag sign at phase 0
+// (E+[L] = BM[L]*2^S + 2^j, viterbiACS.cuh:137-142), and the fp32 cores' complementary-label trick needs
+// a sign multiply the int32 core has no one-op form for.  So the phase-0 entries also exist with the +tag
+// in an area after the regions: E+[L] of table index i = 12m + o (o = 0, 1) at dword ALT + i + 2L, written by
+// the same lanes with ds_write_addtid_b32 under an EXEC mask (address M0 + offset + 4 lane: the +2L is the
+// offset) and read as one ds_read_b64 per (t, t+6) pair like the regions.  The regions are then 98 dwords
+// apart (banks 0, 34, 4, 38: still distinct for the four labels' pairs) so table + ALT (1,936 B) fit the
+// 5,120 B of LDS a wave has at 8 waves per SIMD.
+template <bool ALT>
+struct TgTabLT {
+    static constexpr int RW = ALT ? 98 : 104;  // dwords per label region
+    static constexpr int REGION = RW * 4;      // bytes per label region
+    static constexpr int ALT_OFF = 4 * REGION; // bytes: the +tag phase-0 area (ALT)
     static __host__ __device__ constexpr bool pairrow(int) { return false; }
     static __host__ __device__ constexpr int index(int r) { return 12 * (r / 12) + 2 * (r % 6) + (r / 6) % 2; }
     static __host__ __device__ constexpr int row(int r) { return 4 * index(r); }
     // stage (within the group) whose entries table index i holds
     static __host__ __device__ constexpr int stage(int i) { return 12 * (i / 12) + 6 * (i % 2) + (i % 12) / 2; }
-    static constexpr int BYTES = 4 * REGION;
+    static constexpr int BYTES = 4 * REGION + (ALT ? 4 * (12 * 7 + 8) : 0);
 };
+using TgTabL = TgTabLT<false>;
 static_assert(TgTabL::stage(TgTabL::index(95)) == 95 && TgTabL::index(TgTabL::stage(64)) == 64, "index <-> stage");
+static_assert(TgTabLT<true>::ALT_OFF % 8 == 0, "ALT pairs are ds_read_b64 aligned");
 // ds_write_addtid_b32 x4: LDS[M0 + OFF + k R + 4 lane] = v_k for the active lanes.  M0 is a register the
 // compiler reserves (it does not honour an "m0" clobber), so the statement saves and restores it.
 template <int OFF, int R>
@@ -123,16 +137,20 @@ __device__ __forceinline__ void lds_write_addtid4(uint32_t base, float v0, float
                  : "memory");
 }
 
-// Survivor ring slots per wave minus one (words traced per traceback batch): table + ring + guards of 4
-// waves (19,136 B; SOFT16 20,160 B) fit 8 workgroups per CU, so every SIMD holds 8 waves (<= 64 VGPRs): 1.4 % faster per
-// batch than 13 slots at 7 waves (profiles/r02/benchab_8w.log), the shorter traceback batches included.
-constexpr int kTbs = 11;
+// Survivor ring: as many 256-B slots as fit next to the table in a wave's 5,120 B (8 workgroups of 4 waves
+// per CU, so every SIMD holds 8 waves at <= 64 VGPRs); one traceback batch traces (slots - 1) words, and
+// its VALU instructions cost the same whatever the number of words, so the longest ring is the cheapest:
+// 13 slots with the fp32 cores' label-region table (1,664 B), 12 with SOFT16's (1,936 B) or the
+// interleaved-row table (1,920 B).  8 waves beat 7 with a longer ring by 1.4 % per batch
+// (profiles/r02/benchab_8w.log).
 constexpr int kGuardWords = 4;                 // guard words before the table, between table and ring, after the ring
 constexpr uint32_t kGuardPattern = 0xA5C3E10Fu;
+constexpr int kWaveLdsWords = 163840 / 4 / (8 * kWaves);  // 1,280: a wave's share at 8 workgroups per CU
 template <int TABB, int GW = kGuardWords>
 struct TgLds {
     static constexpr int TAB = TABB / 4;                   // table words
-    static constexpr int RING = (kTbs + 1) * 64;           // ring words
+    static constexpr int TBS = (kWaveLdsWords - 3 * GW - TAB) / 64 - 1;  // words per traceback batch
+    static constexpr int RING = (TBS + 1) * 64;            // ring words
     static constexpr int TAB_OFF = GW;                     // word offsets within a wave's part
     static constexpr int RING_OFF = 2 * GW + TAB;
     static constexpr int WAVE = 3 * GW + TAB + RING;
@@ -142,7 +160,10 @@ struct TgLds {
         return i < GW ? i : i < 2 * GW ? TAB + i : TAB + RING + i;
     }
 };
-static_assert(kWaves * TgLds<TgTab<false>::BYTES>::WAVE * 4 <= 20480 && kWaves * TgLds<TgTab<true>::BYTES>::WAVE * 4 <= 20480,
+static_assert(TgLds<TgTabL::BYTES>::TBS == 12 && TgLds<TgTabLT<true>::BYTES>::TBS == 11 && TgLds<TgTab<true>::BYTES>::TBS == 11,
+              "ring lengths");
+static_assert(kWaves * TgLds<TgTab<false>::BYTES>::WAVE * 4 <= 20480 && kWaves * TgLds<TgTab<true>::BYTES>::WAVE * 4 <= 20480 &&
+                  kWaves * TgLds<TgTabLT<true>::BYTES>::WAVE * 4 <= 20480,
               "8 workgroups of 4 waves per CU (160 KiB of LDS)");
 
 __device__ __forceinline__ int tg_pos(int l)
@@ -511,13 +532,14 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t tg_rsrc(const void* in, uint64
 // after 1536 of 4 whole chunks (7 waves per SIMD, round 2's split), or 1792 workgroups of 3 chunks and
 // 256 of 4 (8 waves of 3/4 chunk or 1 chunk per SIMD, their progress kept even by the fairness controller
 // in fractions of their work).
-constexpr int kSplitWarm = 6;                // warm-up blocks of a speculative segment (multiple of 3)
+constexpr int kSplitWarm = 6;                // default warm-up blocks of a speculative segment (Geom::segWarm)
 constexpr int kSplitMinWords = 64;           // chunks of fewer 32-bit words are not split (host side)
 constexpr int kSegSnap = 8;                  // a boundary this close to a chunk start or end moves onto it
 // a workgroup's chunks (at most kWaves) and their 32-bit word counts; wave-uniform, in scalar registers
 struct SegWG {
     uint32_t c0;
     int k;
+    uint32_t warm;  // warm-up blocks of a segment that starts inside a chunk (3 or 6)
     uint32_t W0, W1, W2, W3;
     __host__ __device__ __forceinline__ uint32_t W(int i) const { return i == 0 ? W0 : i == 1 ? W1 : i == 2 ? W2 : W3; }
     __host__ __device__ __forceinline__ uint32_t cum(int i) const  // words of chunks 0 .. i-1
@@ -527,7 +549,7 @@ struct SegWG {
 };
 struct SegPos {
     int i;       // chunk within the workgroup (k: the end)
-    uint32_t a;  // local word; a > 0: (a + 1) % 3 == 0 and a >= kSplitWarm
+    uint32_t a;  // local word; a > 0: (a + 1) % 3 == 0 and a >= kSegSnap > warm
 };
 // boundary q (0 .. kWaves) of the workgroup's segments
 __host__ __device__ __forceinline__ SegPos seg_bound(const SegWG& w, int q)
@@ -555,7 +577,7 @@ __host__ __device__ __forceinline__ RunGeo seg_run(const SegWG& w, SegPos b0, Se
     g.i = b0.i + r;
     const uint32_t a = r == 0 ? b0.a : 0u, W = w.W(g.i);
     const uint32_t b = g.i == b1.i ? b1.a : W;
-    g.s0 = a == 0 ? 0u : a + 1 - kSplitWarm;
+    g.s0 = a == 0 ? 0u : a + 1 - w.warm;
     g.words = b - g.s0;
     g.E = a - g.s0;
     g.Xspec = a == 0 ? -1 : (int)(a + 1 - g.s0);
@@ -579,9 +601,10 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(8))
     // s = -1 in the upper half (v_fma, as cheap as v_add), and the M_B32 table is the M_B16 one.  SOFT16
     // (INT) keeps the pair rows: each lane reads its own tag sign's half.
     constexpr bool S32 = CORE == B32 && !INT;
-    // LR: the label-region table (TgTabL) written with ds_write_addtid_b32 (SOFT16 keeps the pair-row table)
-    constexpr bool LR = !INT && !(ABL & kAblRowTable);
-    using TT = std::conditional_t<LR, TgTabL, TgTab<INT>>;
+    // LR: the label-region table (TgTabLT; SOFT16 with its +tag phase-0 area) written with
+    // ds_write_addtid_b32; kAblRowTable: round 2's interleaved rows (tools A/B)
+    constexpr bool LR = !(ABL & kAblRowTable);
+    using TT = std::conditional_t<LR, TgTabLT<INT>, TgTab<INT>>;
     using LL = TgLds<TT::BYTES, (ABL & kAblNoGuardSpace) ? 0 : kGuardWords>;
     constexpr int J = FMT::J, S = FMT::S;
     __shared__ __attribute__((aligned(16))) uint32_t lds[kWaves * LL::WAVE];
@@ -608,6 +631,7 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(8))
     if (split) {
         sw.c0 = geo.seg[blockIdx.x];
         sw.k = (int)(geo.seg[blockIdx.x + 1] - sw.c0);
+        sw.warm = geo.segWarm;
         sw.W0 = words32(sw.c0);
         sw.W1 = sw.k > 1 ? words32(sw.c0 + 1) : 0u;
         sw.W2 = sw.k > 2 ? words32(sw.c0 + 2) : 0u;
@@ -615,6 +639,7 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(8))
     } else {
         sw.c0 = gchunk - batch * geo.nchunks;
         sw.k = 1;
+        sw.warm = 0u;
         sw.W0 = words32(sw.c0);
         sw.W1 = sw.W2 = sw.W3 = 0u;
         if (sw.W0 == 0) return;  // an empty chunk (never in a segment launch: its chunks have >= kSplitMinWords words)
@@ -630,12 +655,14 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(8))
     // per-lane LDS byte offset of this position's entry in a phase-K row (row offsets are compile-time)
     const bool upper5 = (pos >> 5) & 1;
     int aK[6];
-    constexpr int LSTR = LR ? TgTabL::REGION : 8;  // bytes between the entries of two labels
+    constexpr int LSTR = LR ? TgTabLT<INT>::REGION : 8;  // bytes between the entries of two labels
     sfor<6>([&](auto KK) {
         constexpr int K = decltype(KK)::value;
         aK[K] = LSTR * own_label(pos, K);
     });
     if constexpr (S32) aK[0] = upper5 ? 3 * LSTR - aK[0] : aK[0];  // upper half: the complementary label 3 - L
+    // INT, label regions: the upper half's phase-0 entries come from the +tag area
+    if constexpr (INT && LR) aK[0] = upper5 ? TgTabLT<true>::ALT_OFF + 8 * own_label(pos, 0) : aK[0];
     const float sg0 = upper5 ? -1.0f : 1.0f;                  // S32: sign of the phase-0 entry
     const int aU0 = aK[0] + (upper5 ? 4 : 0);  // INT phase-0 pair row: this lane's (E-, E+) half
     const int pa5 = 4 * (lane ^ 32);           // ds_bpermute address of the xor-32 partner
@@ -701,7 +728,7 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(8))
     if (pass > 0) vS = V;
     const uint32_t j0 = pass == 0 ? 0u : (uint32_t)Xspec;
     uint32_t kb = 0;
-    uint32_t tbn = pass == 0 ? kTbs - 3 * (blockIdx.x & 3) : kTbs;
+    uint32_t tbn = pass == 0 ? LL::TBS - 3 * (blockIdx.x & 3) : LL::TBS;
     __amdgpu_buffer_rsrc_t rs = tg_rsrc<CH>(in, start + 32ull * j0, availB);
     typename IN::raw_t rA = IN::template load<0>(rs, vo1);               // stage sA of the group
     typename IN::raw_t rB = IN::template load<LR ? 0 : 2>(rs, vo2);      // stage sB
@@ -806,7 +833,7 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(8))
             wave_sync();
             ring[pos] = word;  // block j becomes slot 0 of the next batch
             kb = j - 1;
-            tbn = kTbs;
+            tbn = LL::TBS;
         }
         return j + 1 < nblk;
     };
@@ -821,6 +848,13 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(8))
             uint32_t* e = (uint32_t*)(tabb + rb);
             // the tag of the row's own class: -2^j (the int32 core: exchanged wins ties)
             const int a = A * (1 << S), b = B * (1 << S), tag = -(int)tg0;
+            if constexpr (LR) {
+                auto f = [](int x) { return __builtin_bit_cast(float, x); };
+                lds_write_addtid4<256 * part, TT::REGION>(tabl, f(-a - tag), f(-b - tag), f(b - tag), f(a - tag));
+                if (K == 0)  // phase-0 lanes: the +tag entries (ALT), at dword ALT + index + 2L
+                    lds_write_addtid4<TT::ALT_OFF + 256 * part, 8>(tabl, f(-a + tag), f(-b + tag), f(b + tag), f(a + tag));
+                return;
+            }
             e[0] = (uint32_t)(-a - tag);
             e[2] = (uint32_t)(-b - tag);
             e[4] = (uint32_t)(b - tag);

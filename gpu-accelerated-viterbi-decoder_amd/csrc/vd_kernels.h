@@ -45,6 +45,7 @@ struct Geom {
     // segment launch (vd_kernel_tg.h "segment launches"): workgroup g decodes chunks [seg[g], seg[g+1]) as
     // kWaves segments (their boundary vectors stay in the workgroup's LDS); null = one chunk per wave
     const uint32_t* seg = nullptr;
+    uint32_t segWarm = 6;        // warm-up blocks of a segment that starts inside a chunk (a multiple of 3)
     uint32_t* stats = nullptr;   // count of segments re-decoded (or null)
     // LDS guard check (tests): non-null = write guard words around every wave's table and ring and count
     // the ones found overwritten at kernel exit into *check

@@ -1,11 +1,10 @@
-# segment launches: 3-mode single-launch A/B with clock stamps, then the split/guard/stream GPU tests
+# single-launch modes (plain / pieces / thirds, 6 or 3 warm-up blocks): gpurun -- bash scripts/gpu_seg.sh <tag>
 set -o pipefail
 cd $GRAFT_REPO_ROOT
-export TMPDIR=/tmp
 O=gpurun_out/${1:-seg}
 mkdir -p $O
-timeout -k 10 120 tools/vd_splitab 10 0.04 > $O/splitab.log 2>&1
-echo splitab_rc=$?
-cat $O/splitab.log | head -30
-timeout -k 10 600 python -u -m pytest tests/test_gpu_split.py tests/test_gpu_guard.py tests/test_gpu_streams.py -x -v -m gpu --timeout 300 --timeout-method thread > $O/tests.log 2>&1
-echo test_rc=$?; tail -3 $O/tests.log; grep -E "FAILED|Error" $O/tests.log | head
+timeout -k 10 300 tools/vd_splitab 10 0.04 > $O/splitab_bsc04.log 2>&1 || { echo rc=$?; cat $O/splitab_bsc04.log; exit 1; }
+cat $O/splitab_bsc04.log
+timeout -k 10 300 tools/vd_splitab 4 0.08 > $O/splitab_bsc08.log 2>&1 || { echo rc=$?; cat $O/splitab_bsc08.log; exit 1; }
+grep -E "exact|median|re-decoded" $O/splitab_bsc08.log
+echo all_rc=0

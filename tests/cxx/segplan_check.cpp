@@ -1,7 +1,7 @@
 // Host check of the segment-launch geometry (vd_kernel_tg.h "segment launches", vd_segplan.h): for both
 // tables and for many chunk-word patterns, the 4 segments of every workgroup cover each word of every
 // chunk exactly once (emitted words), in order; every run starts at a chunk start (exact) or at a word
-// a with (a + 1) % 3 == 0 and a >= kSplitWarm; every speculative start has a left neighbour ending at the
+// a with (a + 1) % 3 == 0 and a >= the warm-up (3 and 6 blocks); every speculative start has a left neighbour ending at the
 // same chunk block (its end vector is recorded at the block the start vector is); no segment is empty.
 // Built with hipcc on the host by tests/test_segplan.py; prints "ok" or the first violation.
 #include <cstdio>
@@ -18,12 +18,13 @@ static int fail(const char* what, int g, int q)
     return 1;
 }
 
-static int check_table(const std::vector<uint32_t>& t, const std::vector<uint32_t>& words)
+static int check_table(const std::vector<uint32_t>& t, const std::vector<uint32_t>& words, uint32_t warm)
 {
     for (size_t g = 0; g + 1 < t.size(); g++) {
         SegWG w;
         w.c0 = t[g];
         w.k = (int)(t[g + 1] - t[g]);
+        w.warm = warm;
         if (w.k < 1 || w.k > kWaves) return fail("chunks per workgroup", (int)g, -1);
         uint32_t W[4] = {0, 0, 0, 0};
         for (int i = 0; i < w.k; i++) W[i] = words[w.c0 + i];
@@ -41,7 +42,7 @@ static int check_table(const std::vector<uint32_t>& t, const std::vector<uint32_
                 if (rg.i < 0 || rg.i >= w.k) return fail("run chunk", (int)g, q);
                 const uint32_t a = rg.s0 + rg.E, b = rg.s0 + rg.words;
                 if (r > 0 && a != 0) return fail("later run not at a chunk start", (int)g, q);
-                if (a > 0 && ((a + 1) % 3 != 0 || a < (uint32_t)kSplitWarm || rg.s0 % 3 != 0))
+                if (a > 0 && ((a + 1) % 3 != 0 || a < warm || rg.s0 % 3 != 0))
                     return fail("speculative start alignment", (int)g, q);
                 if ((rg.Xspec >= 0) != (a > 0)) return fail("Xspec", (int)g, q);
                 if (rg.Xspec >= 0 && (uint32_t)rg.Xspec + rg.s0 != a + 1) return fail("Xspec block", (int)g, q);
@@ -77,7 +78,7 @@ int main()
         for (uint32_t pack : packs) {
             std::vector<uint32_t> words(kChunks);
             for (uint32_t c = 0; c < (uint32_t)kChunks; c++) words[c] = pack / kChunks + (c < pack % kChunks ? 1 : 0);
-            bad |= check_table(t, words);
+            for (uint32_t warm : {3u, 6u}) bad |= check_table(t, words, warm);
         }
     }
     if (!bad) printf("ok\n");

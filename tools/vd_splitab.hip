@@ -45,12 +45,15 @@ int main(int argc, char** argv)
     uint32_t* stats;
     CK(hipMalloc(&stats, 4));
     CK(hipMemset(stats, 0, 4));
-    // mode 0: plain; 1: pieces; 2: thirds
-    const char* names[3] = {"plain", "pieces", "thirds"};
-    uint32_t* tab[3] = {nullptr, nullptr, nullptr};
-    unsigned grid[3] = {1600, 0, 0};
-    for (int m = 1; m < 3; m++) {
-        std::vector<uint32_t> t = vd::seg_table(4 * cus, m == 2);
+    // modes: plain; pieces and thirds with 6 and 3 warm-up blocks per speculative segment
+    constexpr int NM = 5;
+    const char* names[NM] = {"plain", "pieces", "pieces-w3", "thirds", "thirds-w3"};
+    const bool thirdsOf[NM] = {false, false, false, true, true};
+    const uint32_t warmOf[NM] = {0, 6, 3, 6, 3};
+    uint32_t* tab[NM] = {nullptr};
+    unsigned grid[NM] = {1600, 0, 0, 0, 0};
+    for (int m = 1; m < NM; m++) {
+        std::vector<uint32_t> t = vd::seg_table(4 * cus, thirdsOf[m]);
         if (t.empty()) { printf("no %s table for %d CUs\n", names[m], cus); return 1; }
         CK(hipMalloc(&tab[m], t.size() * 4));
         CK(hipMemcpy(tab[m], t.data(), t.size() * 4, hipMemcpyHostToDevice));
@@ -58,14 +61,14 @@ int main(int argc, char** argv)
     }
     auto launch = [&](KFn f, int m) {
         vd::Geom q = g;
-        if (m) { q.seg = tab[m]; q.stats = stats; }
+        if (m) { q.seg = tab[m]; q.stats = stats; q.segWarm = warmOf[m]; }
         hipLaunchKernelGGL(f, dim3(grid[m]), dim3(256), 0, 0, in, out, q);
     };
     KFn f0 = (KFn)vd::vd_decode_tg<vd::HARD, vd::B32, 32, 0>, fc = (KFn)vd::vd_decode_tg<vd::HARD, vd::B32, 32, vd::kAblClock>;
     // the modes decode the same words
     {
         std::vector<uint32_t> a(g.packNum), b(g.packNum);
-        for (int m = 0; m < 3; m++) {
+        for (int m = 0; m < NM; m++) {
             CK(hipMemset(out, 0, g.packNum * 4));
             launch(f0, m);
             CK(hipMemcpy(m ? b.data() : a.data(), out, g.packNum * 4, hipMemcpyDeviceToHost));
@@ -79,23 +82,29 @@ int main(int argc, char** argv)
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
     const int rounds = argc > 1 ? atoi(argv[1]) : 10;
-    std::vector<float> t[3], tb[3];
+    std::vector<float> t[NM], tb[NM];
     for (int r = 0; r < rounds + 2; r++)
-        for (int m = 0; m < 3; m++) {
+        for (int m = 0; m < NM; m++) {
             CK(hipEventRecord(e0)); launch(f0, m); CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
             float ms; CK(hipEventElapsedTime(&ms, e0, e1)); if (r >= 2) t[m].push_back(ms);
             // back to back (as a caller streams batches): 20 launches between two events
             CK(hipEventRecord(e0)); for (int k = 0; k < 20; k++) launch(f0, m); CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
             CK(hipEventElapsedTime(&ms, e0, e1)); if (r >= 2) tb[m].push_back(ms / 20);
         }
-    for (int m = 0; m < 3; m++) {
+    for (int m = 0; m < NM; m++) {
         std::sort(t[m].begin(), t[m].end()); std::sort(tb[m].begin(), tb[m].end());
         printf("%-7s isolated median %.4f ms  back to back (20) median %.4f ms per launch -> %.1f Gb/s\n", names[m],
                t[m][t[m].size() / 2], tb[m][tb[m].size() / 2], (double)(N - 64) / (tb[m][tb[m].size() / 2] * 1e-3) / 1e9);
     }
     uint32_t redec = 0; CK(hipMemcpy(&redec, stats, 4, hipMemcpyDeviceToHost));
     printf("re-decoded segments over all segment launches: %u\n", redec);
-    for (int m = 0; m < 3; m++) {
+    for (int m = 1; m < NM; m++) {  // re-decodes per launch by mode
+        CK(hipMemset(stats, 0, 4));
+        for (int k = 0; k < 10; k++) launch(f0, m);
+        CK(hipMemcpy(&redec, stats, 4, hipMemcpyDeviceToHost));
+        printf("  %-9s re-decoded segments in 10 launches: %u\n", names[m], redec);
+    }
+    for (int m = 0; m < NM; m++) {
         const int nw = (int)grid[m] * 4;
         for (int r = 0; r < 3; r++) launch(fc, m);
         CK(hipDeviceSynchronize());
