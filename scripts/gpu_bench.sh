@@ -1,0 +1,14 @@
+# smoke(), the driver's bench command, and the same command under rocprofv3 --kernel-trace --stats:
+# gpurun --timeout 1100 -- bash scripts/gpu_bench.sh <tag>
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+O=gpurun_out/${1:-bench}
+mkdir -p $O
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $O/smoke.log 2>&1 || { echo smoke_rc=$?; tail $O/smoke.log; exit 1; }
+timeout -k 10 400 python bench.py > $O/bench.log 2> $O/bench.err || { echo bench_rc=$?; tail $O/bench.err; exit 1; }
+tail -1 $O/bench.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); c=d['config']; print(d['value'], d['ms_per_step'], c['kernel_ms'], {k: v['gbps'] for k, v in c['other_configs'].items()}, c['single_launch'], c['llr_input']['fused_batched'], c['final_gather']['checksums_match'], d['cpu_baseline']['matches_gpu'])"
+timeout -k 10 500 rocprofv3 --kernel-trace --stats -d $O/trace -o run --output-format csv -- python bench.py > $O/trace.log 2>&1 || { echo trace_rc=$?; tail $O/trace.log; exit 1; }
+find $O/trace -name "*kernel_stats.csv" -exec cp {} $O/kernel_stats.csv \;
+head -6 $O/kernel_stats.csv
+echo all_rc=0

@@ -49,6 +49,12 @@ int main(int argc, char** argv)
         const uint32_t s0 = q8((o0[t] ? -1.0 : 1.0) + G(rng)), s1 = q8((o1[t] ? -1.0 : 1.0) + G(rng));
         hs[t / 2] |= ((s0 << 8) | s1) << (16 * ((t % 2) ^ 1));
     }
+    // FP32 input (2 floats per stage): BPSK + AWGN at 2 dB, unscaled (the kernel clamps to [-8, 7])
+    std::vector<float> hf(2 * N + 128, 0.0f);
+    for (size_t t = 0; t < N; t++) {
+        hf[2 * t] = (float)((o0[t] ? -1.0 : 1.0) + G(rng)) * 4.0f;
+        hf[2 * t + 1] = (float)((o1[t] ? -1.0 : 1.0) + G(rng)) * 4.0f;
+    }
     vd::Geom g{};
     g.packNum = (N - 64) / 32;
     g.nchunks = 6400;
@@ -128,6 +134,33 @@ int main(int argc, char** argv)
         }
         const double m = (double)ns.size(), b = (m * sxy - sx * sy) / (m * sxx - sx * sx), a = (sy - b * sx) / m;
         printf("  fit %s: t(n) = %.4f + %.4f / n ms (per-launch ramp + tail %.1f us)\n", w ? "soft8" : "hard ", a, b, b * 1e3);
+    }
+    // (3) FP32 input (8 B per stage): `steps` distinct resident batches against one batch read `steps` times
+    //     (input stride 0: after the first batch it comes from the caches), SOFT8 alongside
+    {
+        const size_t strF = (hf.size() * 4 + 255) / 256 * 256;
+        char* bF;
+        CK(hipMalloc(&bF, strF * steps));
+        for (int k = 0; k < steps; k++) CK(hipMemcpy(bF + k * strF, hf.data(), hf.size() * 4, hipMemcpyHostToDevice));
+        const KFn kf = (KFn)vd::vd_decode_tg<vd::FP32, vd::F16, 32, 0>;
+        std::vector<float> tf[3];
+        for (int r = 0; r < rounds; r++)
+            for (int v = 0; v < 3; v++) {
+                vd::Geom q = g;
+                q.nbatch = (uint32_t)steps;
+                q.outStride = ostr;
+                q.inStride = v == 0 ? strF : v == 1 ? 0 : strS;
+                CK(hipEventRecord(e0));
+                hipLaunchKernelGGL(v < 2 ? kf : ks, dim3(1600u * steps), dim3(256), 0, 0, v < 2 ? bF : bS, bO, q);
+                CK(hipEventRecord(e1));
+                CK(hipEventSynchronize(e1));
+                float ms;
+                CK(hipEventElapsedTime(&ms, e0, e1));
+                tf[v].push_back(ms / steps);
+            }
+        printf("(3) %d-batch launches, ms per batch: fp32/f16 distinct inputs %.4f, fp32/f16 one input (stride 0) %.4f, soft8/b16 distinct %.4f\n",
+               steps, median(tf[0]), median(tf[1]), median(tf[2]));
+        CK(hipFree(bF));
     }
     return 0;
 }
