@@ -46,6 +46,7 @@ constexpr int kAblNoTraceback = 1, kAblNoTabReads = 2, kAblNoReadout = 4, kAblNo
               kAblClock = 32, kAblNoFair = 256, kAblNoTabWrites = 512, kAblNoGuardSpace = 1024;
 // layout variants (tools A/B; exact twins of the product)
 constexpr int kAblRowTable = 2048;  // fp32 cores: the interleaved-row table (TgTab) written with ds_write2_b32
+constexpr int kAblTbPerWord = 4096;  // traceback constants computed per word, not once per lane (round 2)
 constexpr int kAblAcsOnly = kAblNoTraceback | kAblNoTabReads | kAblNoReadout | kAblNoTabBuild | kAblNoLoads;
 
 template <int CH>
@@ -262,41 +263,86 @@ __device__ __forceinline__ void tg_stage_lds_i(float& V, float m, float vp)
 // of (bits ^ T << (J-6)) and the state at the field start is its low 6 bits.  M_B32 keeps its raw
 // phase-0 bits (own-wins tag in the upper position half), which already are the decoded bits there.
 // One dependent LDS read per J stages instead of one per stage.
+//
+// Constants of the traceback of word k: they depend on the stage phase of its emit block,
+// ph = 2 ((k + 1) % 3), only: the bit offsets (+ J - 6, see below) of the position of a state at the three
+// odd field-end phases, and (M_B32) the phase-0 mask of field-start phase ph.  When every traceback batch
+// starts at a multiple of 3 words, ph is the lane's (k = kb + lane): tb_pack(lane) computes the constants
+// once per kernel into 5-bit fields of one word, tb_unpack reads them back.
+struct TbC {
+    uint32_t off[3];
+    uint32_t m50;
+};
 template <int J, bool FIX5>
-__device__ __forceinline__ uint32_t traceback_word_tg(const char* ringb, uint32_t slot1, uint32_t k)
+__device__ __forceinline__ TbC tb_direct(int k)
+{
+    const int ph = 2 * ((k + 1) % 3);
+    TbC c;
+    c.off[0] = 5 - ph + J - 6;
+    c.off[1] = (ph <= 2 ? 3 - ph : 9 - ph) + J - 6;
+    c.off[2] = (ph == 0 ? 1 : 7 - ph) + J - 6;
+    c.m50 = FIX5 ? 0x41041041u << ((12 - ph) % 6) : 0u;
+    return c;
+}
+template <int J, bool FIX5>
+__device__ __forceinline__ uint32_t tb_pack(int lane)
+{
+    const int ph = 2 * ((lane + 1) % 3);
+    const TbC c = tb_direct<J, false>(lane);
+    return c.off[0] | c.off[1] << 5 | c.off[2] << 10 | (FIX5 ? (uint32_t)((12 - ph) % 6) << 15 : 0u);
+}
+template <bool FIX5>
+__device__ __forceinline__ TbC tb_unpack(uint32_t tbk)
+{
+    TbC c;  // v_bfe_u32 takes its offset from bits 4:0 of the operand
+    c.off[0] = tbk;
+    c.off[1] = tbk >> 5;
+    c.off[2] = tbk >> 10;
+    c.m50 = FIX5 ? 0x41041041u << ((tbk >> 15) & 31u) : 0u;
+    return c;
+}
+template <int J, bool FIX5>
+__device__ __forceinline__ uint32_t traceback_word_tg(const char* ringb, uint32_t slot1, const TbC& tc)
 {
     constexpr int G = 32 / J;
-    const int ph = (int)(2 * ((k + 1) % 3));  // stage phase of the emit block's first stage (even)
-    // position of state T at a field end of stage phase s (odd) is rotl6(T, s) = (T*65 >> (6-s)) & 63
-    int off[3];  // by s = (ph + c) % 6 for c = 1, 3, 5
-    off[0] = 5 - ph;
-    off[1] = ph <= 2 ? 3 - ph : 9 - ph;
-    off[2] = ph == 0 ? 1 : 7 - ph;
+    // position of state T at a field end of stage phase s (odd) is rotl6(T, s) = bits [6-s, 12-s) of
+    // T | T << 6.  TX = T * (2^(J-6) + 2^J) holds that pair shifted by J - 6: its bits [J-6, J) are the
+    // T << (J-6) the field's XOR needs, so one multiply serves both (the copy above bit J is masked off
+    // below).
+    const uint32_t* const off = tc.off;
     uint32_t m5[3] = {0u, 0u, 0u};  // M_B32: bits of phase-0 stages for field start phase ph + 2d
     if constexpr (FIX5) {
-        sfor<3>([&](auto D) {
-            constexpr int d = decltype(D)::value;
-            m5[d] = 0x41041041u << ((12 - ph - 2 * d) % 6);
-        });
+        // 0x41041041 << ((12 - ph - 2d) % 6).  The mask has period 6, so in bits 0..29 (a field has J <= 16)
+        // a shift by (s - 2) mod 6 is a right shift by 2 of the shift by s, whatever s in {0, 2, 4}.
+        m5[0] = tc.m50;
+        m5[1] = m5[0] >> 2;
+        m5[2] = m5[0] >> 4;
     }
+    constexpr uint32_t JM = (1u << J) - 1u;
     uint32_t T = 0, nat = 0;
     auto field = [&](auto BOc, auto Gc, uint32_t slot) {
         constexpr int BO = decltype(BOc)::value;  // 0: emit block, 2: convergence block
         constexpr int g = decltype(Gc)::value;
         constexpr int c = (BO + J * g + J - 1) % 6;
-        const uint32_t p = __builtin_amdgcn_ubfe(T * 65u, (uint32_t)off[c / 2], 6u);
+        const uint32_t TX = T * ((1u << (J - 6)) | (1u << J));
+        const uint32_t p = __builtin_amdgcn_ubfe(TX, off[c / 2], 6u);
         uint32_t W;
         if constexpr (J == 8) W = *(const uint8_t*)(ringb + slot + 4 * p + g);
         else W = *(const uint16_t*)(ringb + slot + 4 * p + 2 * g);
-        uint32_t Y = W ^ (T << (J - 6));
-        Y ^= Y >> 6;
-        if constexpr (J == 16) Y ^= Y >> 12;
+        // the stride-6 suffix XOR of the field's J bits of W ^ T << (J-6) (bits >= J of Y: the copy of T)
+        uint32_t Y = W ^ TX;
+        if constexpr (J == 8) {
+            Y ^= __builtin_amdgcn_ubfe(Y, 6u, 2u);
+        } else {
+            Y ^= __builtin_amdgcn_ubfe(Y, 6u, 10u);
+            Y ^= __builtin_amdgcn_ubfe(Y, 12u, 4u);
+        }
         if constexpr (FIX5) {
             constexpr int d = ((BO + J * g) % 6) / 2;
             Y = (m5[d] & W) | (~m5[d] & Y);
         }
         T = Y & 63u;
-        return Y;
+        return Y & JM;
     };
     sfor<G>([&](auto I) {  // convergence: block k+2, fields G-1 .. 0
         constexpr int g = G - 1 - decltype(I)::value;
@@ -666,6 +712,7 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(8))
     const float sg0 = upper5 ? -1.0f : 1.0f;                  // S32: sign of the phase-0 entry
     const int aU0 = aK[0] + (upper5 ? 4 : 0);  // INT phase-0 pair row: this lane's (E-, E+) half
     const int pa5 = 4 * (lane ^ 32);           // ds_bpermute address of the xor-32 partner
+    const uint32_t tbk = tb_pack<J, CORE == B32>(lane);  // traceback constants of word kb + lane (kb % 3 == 0)
     // table-build roles: every lane writes row `lane` (stages 0..63 of the group), lanes 0..31 also
     // row 64 + lane; J divides 32, so the tag position (row % J) is lane % J for both.  (Writing rows
     // 0..59 of the next group a block ahead, when they are dead, measured no faster:
@@ -791,7 +838,7 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(8))
 #define VD_TG_RO(SEL, UNUSED) "v_lshrrev_b32_sdwa %[w], 1, %[V] dst_sel:" SEL " dst_unused:" UNUSED             \
                               " src0_sel:DWORD src1_sel:DWORD\n\tv_and_or_b32 %[V], %[V], %[fnm], %[fhf]"
 #define VD_TG_RN "\n\ts_nop 0\n\tv_readfirstlane_b32 %[sr], %[V]\n\ts_sub_u32 %[sr], %[sr], %[vb]\n\tv_subrev_u32 %[V], %[sr], %[V]"
-#define VD_TG_IN [fnm] "v"(fnm), [fhf] "v"(fhf), [vb] "n"(VBASE)
+#define VD_TG_IN [fnm] "v"(fnm), [fhf] "s"(fhf), [vb] "n"(VBASE)  // fhf on the constant bus: one VGPR fewer
                 if constexpr (J == 8 && g == 0)
                     asm(VD_TG_RO("BYTE_0", "UNUSED_PAD") : [V] "+{v60}"(V), [w] "=&v"(word) : VD_TG_IN);
                 else if constexpr (J == 8 && g == 1)
@@ -820,7 +867,13 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(8))
             const uint32_t nw = j - 1 - kb;
             if (!(ABL & kAblNoTraceback) && (uint32_t)lane < nw && kb + lane >= E) {
                 const uint32_t k = kb + (uint32_t)lane;
-                uint32_t w = traceback_word_tg<J, CORE == B32>((const char*)ring, (uint32_t)(lane + 1) * 256u, k);
+                // with TBS a multiple of 3 (12: the fp32 cores' label-region table) every batch starts at a
+                // multiple of 3 (batches of TBS - 3 (blockIdx.x & 3) or TBS words), so word k's phase follows
+                // from the lane; otherwise (SOFT16: 11) from k.  The M_B32 kernels have no VGPR to keep the
+                // lane's constants in (64 at 8 waves per SIMD) and compute them here.
+                const TbC tc = LL::TBS % 3 == 0 && CORE != B32 && !(ABL & kAblTbPerWord) ? tb_unpack<CORE == B32>(tbk)
+                                                                                          : tb_direct<J, CORE == B32>((int)k);
+                uint32_t w = traceback_word_tg<J, CORE == B32>((const char*)ring, (uint32_t)(lane + 1) * 256u, tc);
                 if constexpr (OB == 32) {
                     ((uint32_t*)out)[wOut + k] = w;
                 } else {
