@@ -47,6 +47,7 @@ constexpr int kAblNoTraceback = 1, kAblNoTabReads = 2, kAblNoReadout = 4, kAblNo
 // layout variants (tools A/B; exact twins of the product)
 constexpr int kAblRowTable = 2048;  // fp32 cores: the interleaved-row table (TgTab) written with ds_write2_b32
 constexpr int kAblTbPerWord = 4096;  // traceback constants computed per word, not once per lane (round 2)
+constexpr int kAblPostExchange = 8192;  // LDS-exchange stages exchange V and subtract after (round 2)
 constexpr int kAblAcsOnly = kAblNoTraceback | kAblNoTabReads | kAblNoReadout | kAblNoTabBuild | kAblNoLoads;
 
 template <int CH>
@@ -222,6 +223,23 @@ __device__ __forceinline__ void tg_stage_lds(float& V, float m, float vp)
     float t1, t2;
     asm("v_add_f32 %1, %0, %3\n\tv_sub_f32 %2, %4, %3\n\tv_max_f32 %0, %1, %2"
         : "+{v60}"(V), "=&v"(t1), "=&v"(t2) : "v"(m), "v"(vp));
+}
+// The same stage with the subtraction before the exchange: b = V - m goes through the LDS crossbar, and
+// since the exchange partners share the label and the tag (every core, except the M_B32 phase-0 stage
+// with its per-half tag sign), the received value is V_partner - m.  After the exchange returns only the
+// max is left, so the round trip's dependent chain is one op shorter; a = V + m issues while it is in
+// flight.
+template <bool X32, bool INT>
+__device__ __forceinline__ void tg_stage_lds_pre(float& V, float m, int paddr)
+{
+    float a, b;
+    if constexpr (INT) asm("v_sub_u32 %0, %1, %2" : "=v"(b) : "v"(V), "v"(m));
+    else asm("v_sub_f32 %0, %1, %2" : "=v"(b) : "v"(V), "v"(m));
+    const float bp = X32 ? tg_partner(b, paddr) : tg_swz16(b);
+    if constexpr (INT) asm("v_add_u32 %0, %1, %2" : "=v"(a) : "v"(V), "v"(m));
+    else asm("v_add_f32 %0, %1, %2" : "=v"(a) : "v"(V), "v"(m));
+    if constexpr (INT) asm("v_max_i32 %0, %1, %2" : "={v60}"(V) : "v"(a), "v"(bp));
+    else asm("v_max_f32 %0, %1, %2" : "={v60}"(V) : "v"(a), "v"(bp));
 }
 // M_B32 phase-0 stage (S32): V' = max(V + s*m, vp - s*m), s = -1 in the upper position half, where m is
 // the entry of the complementary label (see the kernel)
@@ -647,6 +665,7 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(8))
     // s = -1 in the upper half (v_fma, as cheap as v_add), and the M_B32 table is the M_B16 one.  SOFT16
     // (INT) keeps the pair rows: each lane reads its own tag sign's half.
     constexpr bool S32 = CORE == B32 && !INT;
+    constexpr bool PRE = !(ABL & kAblPostExchange);  // LDS-exchange stages subtract before the exchange
     // LR: the label-region table (TgTabLT; SOFT16 with its +tag phase-0 area) written with
     // ds_write_addtid_b32; kAblRowTable: round 2's interleaved rows (tools A/B)
     constexpr bool LR = !(ABL & kAblRowTable);
@@ -815,13 +834,17 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(8))
             // Q = 0..3: DPP stage (lane xor 1, 2, 7, 8); Q = 4: xor 16 through ds_swizzle; Q = 5: xor 32
             // through ds_bpermute
             if constexpr (INT) {
+                // (SOFT16's phase-0 entries differ in the tag sign between the xor-32 partners: no pre form)
                 if constexpr (Q <= 3) tg_stage_dpp_i2<Q>(V, m);
+                else if constexpr (Q == 4 && PRE) tg_stage_lds_pre<false, true>(V, m, pa5);
                 else if constexpr (Q == 4) tg_stage_lds_i(V, m, tg_swz16(V));
                 else tg_stage_lds_i(V, m, tg_partner(V, pa5));
             } else {
                 if constexpr (Q <= 3) tg_stage_dpp2<Q>(V, m);
+                else if constexpr (Q == 4 && PRE) tg_stage_lds_pre<false, false>(V, m, pa5);
                 else if constexpr (Q == 4) tg_stage_lds(V, m, tg_swz16(V));
                 else if constexpr (S32) tg_stage_lds_sg(V, m, tg_partner(V, pa5), sg0);
+                else if constexpr (PRE) tg_stage_lds_pre<true, false>(V, m, pa5);
                 else tg_stage_lds(V, m, tg_partner(V, pa5));
             }
             if constexpr (r + TGD < 96) issue(std::integral_constant<int, r + TGD>{});

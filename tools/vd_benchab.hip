@@ -80,7 +80,7 @@ int main(int argc, char** argv)
     g.stats = stats;
     const Variant vs[] = {
         {"product (xor-32 by ds_bpermute)", (KFn)vd::vd_decode_tg<vd::HARD, vd::B32, 32, 0>, (KFn)vd::vd_decode_tg<vd::SOFT8, vd::B16, 32, 0>},
-        {"traceback constants per word", (KFn)vd::vd_decode_tg<vd::HARD, vd::B32, 32, vd::kAblTbPerWord>, (KFn)vd::vd_decode_tg<vd::SOFT8, vd::B16, 32, vd::kAblTbPerWord>},
+        {"LDS stages: exchange V, subtract after", (KFn)vd::vd_decode_tg<vd::HARD, vd::B32, 32, vd::kAblPostExchange>, (KFn)vd::vd_decode_tg<vd::SOFT8, vd::B16, 32, vd::kAblPostExchange>},
     };
     const int nv = sizeof(vs) / sizeof(vs[0]);
     // bench conditions (bench.py): each workload's `steps` batches as one batched launch, every batch its
