@@ -43,10 +43,8 @@ constexpr int kLlr = 8;
 // Component ablations (tools/vd_ablate only; the outputs are wrong): the template argument ABL of
 // vd_decode_tg is a set of these bits, 0 in the product.
 constexpr int kAblNoTraceback = 1, kAblNoTabReads = 2, kAblNoReadout = 4, kAblNoTabBuild = 8, kAblNoLoads = 16,
-              kAblClock = 32, kAblNoFair = 256, kAblNoTabWrites = 512, kAblNoGuardSpace = 1024;
-// layout variants (tools A/B; exact twins of the product)
-constexpr int kAblRowTable = 2048;  // fp32 cores: the interleaved-row table (TgTab) written with ds_write2_b32
-constexpr int kAblTbPerWord = 4096;  // traceback constants computed per word, not once per lane (round 2)
+              kAblClock = 32, kAblNoFair = 256, kAblNoTabWrites = 512;
+// layout variant (tools A/B; an exact twin of the product)
 constexpr int kAblPostExchange = 8192;  // LDS-exchange stages exchange V and subtract after (round 2)
 constexpr int kAblAcsOnly = kAblNoTraceback | kAblNoTabReads | kAblNoReadout | kAblNoTabBuild | kAblNoLoads;
 
@@ -69,37 +67,14 @@ struct TgFmt {
 // fits, so |V +- E| < 2^31.  The CLI default SNR 15 (saturated soft values on the codeword: the best
 // path gains BMmax every stage) is in the parity tests; tests/test_metric_range.py checks the bounds.
 
-// Interleaved-row table (round 2's layout, now the kAblRowTable A/B variant; the product uses TgTabL below):
-// per 96-stage group, 16 periods of 6 rows (row K = stage phase); a row holds
-// E[L] = BM[L]*2^S + tag for the four labels L.  Rows K of periods 2m and 2m+1 are interleaved entry by
-// entry, so a lane's entries for stages t and t+6 are one 8-byte ds_read_b64: entry e of row r sits at
-// row(r) + 8e.  The SOFT16 (INT, M_B32) phase-0 rows hold, per label, the pair (E-, E+) of both tag
-// signs (the M_B32 tie rule differs between the position halves there, viterbiACS.cuh:137-142); the fp32
-// cores take M_B32's upper-half phase-0 entries from the ordinary row instead (S32 in the kernel).
-template <bool PAIR0>
-struct TgTab {
-    static __host__ __device__ constexpr bool pairrow(int K) { return PAIR0 && K == 0; }
-    // dword offsets: period pair m at 60m, row K at ks(K) (8 dwords, a pair row 16), padded so the
-    // 32-lane stores of a table build hit (nearly) distinct banks
-    static __host__ __device__ constexpr int ks(int K)
-    {
-        return PAIR0 ? (K == 0 ? 0 : K == 1 ? 18 : K == 2 ? 26 : K == 3 ? 34 : K == 4 ? 44 : 52) : 10 * K;
-    }
-    static __host__ __device__ constexpr int row(int r)
-    {
-        return 4 * (60 * (r / 12) + ks(r % 6) + ((r / 6) % 2) * (pairrow(r % 6) ? 8 : 1));
-    }
-    static constexpr int BYTES = 8 * 60 * 4;
-};
 // Label-region table (the fp32 cores' table): one region of 96 entries per label, entry of stage
 // t = 12m + 6o + K (period pair m, period o, phase K) at index 12m + 2K + o, so the entries of stages t and
 // t+6 (o = 0, 1) are one ds_read_b64; the regions are 104 dwords apart (banks 0, 40, 16, 56: the four
 // labels' reads in a lane group never share a bank).  Lane l builds the entries of the stage at index l
 // (and lanes 0..31 index 64 + l) and writes them with ds_write_addtid_b32 (address = M0 + offset + 4 lane,
 // no address VGPR: 2 cycles of the store path per 256 B instead of 6 per 512 B for ds_write2_b32 at
-// scattered row addresses).  Against the interleaved-row table (TgTab, kAblRowTable): HARD 0.1627 ->
-// 0.1582 ms, SOFT8 0.1655 -> 0.1632 ms per batch under bench conditions, exact twins
-// (profiles/r03/benchab_label_regions.log).
+// scattered row addresses).  Against round 2's interleaved-row table: HARD 0.1627 -> 0.1582 ms, SOFT8
+// 0.1655 -> 0.1632 ms per batch under bench conditions, exact twins (profiles/r03/benchab_label_regions.log).
 // ALT (SOFT16, int32 patterns): the M_B32 upper position half needs the other tag sign at phase 0
 // (E+[L] = BM[L]*2^S + 2^j, viterbiACS.cuh:137-142), and the fp32 cores' complementary-label trick needs
 // a sign multiply the int32 core has no one-op form for.  So the phase-0 entries also exist with the +tag
@@ -113,7 +88,6 @@ struct TgTabLT {
     static constexpr int RW = ALT ? 98 : 104;  // dwords per label region
     static constexpr int REGION = RW * 4;      // bytes per label region
     static constexpr int ALT_OFF = 4 * REGION; // bytes: the +tag phase-0 area (ALT)
-    static __host__ __device__ constexpr bool pairrow(int) { return false; }
     static __host__ __device__ constexpr int index(int r) { return 12 * (r / 12) + 2 * (r % 6) + (r / 6) % 2; }
     static __host__ __device__ constexpr int row(int r) { return 4 * index(r); }
     // stage (within the group) whose entries table index i holds
@@ -142,14 +116,14 @@ __device__ __forceinline__ void lds_write_addtid4(uint32_t base, float v0, float
 // Survivor ring: as many 256-B slots as fit next to the table in a wave's 5,120 B (8 workgroups of 4 waves
 // per CU, so every SIMD holds 8 waves at <= 64 VGPRs); one traceback batch traces (slots - 1) words, and
 // its VALU instructions cost the same whatever the number of words, so the longest ring is the cheapest:
-// 13 slots with the fp32 cores' label-region table (1,664 B), 12 with SOFT16's (1,936 B) or the
-// interleaved-row table (1,920 B).  8 waves beat 7 with a longer ring by 1.4 % per batch
+// 13 slots with the fp32 cores' label-region table (1,664 B), 12 with SOFT16's (1,936 B).  8 waves beat 7 with a longer ring by 1.4 % per batch
 // (profiles/r02/benchab_8w.log).
 constexpr int kGuardWords = 4;                 // guard words before the table, between table and ring, after the ring
 constexpr uint32_t kGuardPattern = 0xA5C3E10Fu;
 constexpr int kWaveLdsWords = 163840 / 4 / (8 * kWaves);  // 1,280: a wave's share at 8 workgroups per CU
-template <int TABB, int GW = kGuardWords>
+template <int TABB>
 struct TgLds {
+    static constexpr int GW = kGuardWords;
     static constexpr int TAB = TABB / 4;                   // table words
     static constexpr int TBS = (kWaveLdsWords - 3 * GW - TAB) / 64 - 1;  // words per traceback batch
     static constexpr int RING = (TBS + 1) * 64;            // ring words
@@ -162,10 +136,8 @@ struct TgLds {
         return i < GW ? i : i < 2 * GW ? TAB + i : TAB + RING + i;
     }
 };
-static_assert(TgLds<TgTabL::BYTES>::TBS == 12 && TgLds<TgTabLT<true>::BYTES>::TBS == 11 && TgLds<TgTab<true>::BYTES>::TBS == 11,
-              "ring lengths");
-static_assert(kWaves * TgLds<TgTab<false>::BYTES>::WAVE * 4 <= 20480 && kWaves * TgLds<TgTab<true>::BYTES>::WAVE * 4 <= 20480 &&
-                  kWaves * TgLds<TgTabLT<true>::BYTES>::WAVE * 4 <= 20480,
+static_assert(TgLds<TgTabL::BYTES>::TBS == 12 && TgLds<TgTabLT<true>::BYTES>::TBS == 11, "ring lengths");
+static_assert(kWaves * TgLds<TgTabL::BYTES>::WAVE * 4 <= 20480 && kWaves * TgLds<TgTabLT<true>::BYTES>::WAVE * 4 <= 20480,
               "8 workgroups of 4 waves per CU (160 KiB of LDS)");
 
 __device__ __forceinline__ int tg_pos(int l)
@@ -666,11 +638,9 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(8))
     // (INT) keeps the pair rows: each lane reads its own tag sign's half.
     constexpr bool S32 = CORE == B32 && !INT;
     constexpr bool PRE = !(ABL & kAblPostExchange);  // LDS-exchange stages subtract before the exchange
-    // LR: the label-region table (TgTabLT; SOFT16 with its +tag phase-0 area) written with
-    // ds_write_addtid_b32; kAblRowTable: round 2's interleaved rows (tools A/B)
-    constexpr bool LR = !(ABL & kAblRowTable);
-    using TT = std::conditional_t<LR, TgTabLT<INT>, TgTab<INT>>;
-    using LL = TgLds<TT::BYTES, (ABL & kAblNoGuardSpace) ? 0 : kGuardWords>;
+    // the label-region table (TgTabLT; SOFT16 with its +tag phase-0 area) written with ds_write_addtid_b32
+    using TT = TgTabLT<INT>;
+    using LL = TgLds<TT::BYTES>;
     constexpr int J = FMT::J, S = FMT::S;
     __shared__ __attribute__((aligned(16))) uint32_t lds[kWaves * LL::WAVE];
     const int lane = threadIdx.x & 63;
@@ -713,36 +683,32 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(8))
     const SegPos b0 = split ? seg_bound(sw, wv) : SegPos{0, 0u}, b1 = split ? seg_bound(sw, wv + 1) : SegPos{1, 0u};
     const int nrun = seg_nruns(b0, b1);
     // guard words (Geom::check): a uniform branch, nothing when off
-    if (geo.check && lane < 3 * kGuardWords && LL::WAVE != LL::TAB + LL::RING) wlds[LL::guard(lane)] = kGuardPattern;
+    if (geo.check && lane < 3 * kGuardWords) wlds[LL::guard(lane)] = kGuardPattern;
     const uint64_t t_clk0 = (ABL & kAblClock) ? __builtin_amdgcn_s_memtime() : 0;
     const uint64_t t_rt0 = (ABL & kAblClock) ? __builtin_amdgcn_s_memrealtime() : 0;
 
     // per-lane LDS byte offset of this position's entry in a phase-K row (row offsets are compile-time)
     const bool upper5 = (pos >> 5) & 1;
     int aK[6];
-    constexpr int LSTR = LR ? TgTabLT<INT>::REGION : 8;  // bytes between the entries of two labels
+    constexpr int LSTR = TT::REGION;  // bytes between the entries of two labels
     sfor<6>([&](auto KK) {
         constexpr int K = decltype(KK)::value;
         aK[K] = LSTR * own_label(pos, K);
     });
     if constexpr (S32) aK[0] = upper5 ? 3 * LSTR - aK[0] : aK[0];  // upper half: the complementary label 3 - L
     // INT, label regions: the upper half's phase-0 entries come from the +tag area
-    if constexpr (INT && LR) aK[0] = upper5 ? TgTabLT<true>::ALT_OFF + 8 * own_label(pos, 0) : aK[0];
+    if constexpr (INT) aK[0] = upper5 ? TgTabLT<true>::ALT_OFF + 8 * own_label(pos, 0) : aK[0];
     const float sg0 = upper5 ? -1.0f : 1.0f;                  // S32: sign of the phase-0 entry
-    const int aU0 = aK[0] + (upper5 ? 4 : 0);  // INT phase-0 pair row: this lane's (E-, E+) half
     const int pa5 = 4 * (lane ^ 32);           // ds_bpermute address of the xor-32 partner
     const uint32_t tbk = tb_pack<J, CORE == B32>(lane);  // traceback constants of word kb + lane (kb % 3 == 0)
-    // table-build roles: every lane writes row `lane` (stages 0..63 of the group), lanes 0..31 also
-    // row 64 + lane; J divides 32, so the tag position (row % J) is lane % J for both.  (Writing rows
-    // 0..59 of the next group a block ahead, when they are dead, measured no faster:
-    // profiles/r02/ablate_twe.log.)
+    // table-build roles: lane l builds the entries at table index l (stage sA) and, lanes 0..31, index
+    // 64 + l (stage sB).  (Writing a group's entries a block ahead, when they are dead, measured no
+    // faster: profiles/r02/ablate_twe.log.)
     const uint64_t li = (uint64_t)(lane & 31);
-    // LR: lane l builds the entries at table index l (stage sA) and, lanes 0..31, index 64 + l (stage sB)
-    const int sA = LR ? TgTabL::stage(lane) : lane, sB = LR ? TgTabL::stage(64 + (int)li) : 64 + (int)li;
+    const int sA = TgTabL::stage(lane), sB = TgTabL::stage(64 + (int)li);
     const float tagv = (float)(1 << (sA % J)), tagvB = (float)(1 << (sB % J));
     const float tg0A = CORE == F16 ? tagv : -tagv;  // tag of the row's own class (stage sA)
     const float tg0B = CORE == F16 ? tagvB : -tagvB;
-    const int rowb1 = LR ? 0 : TT::row(lane), rowb2 = LR ? 0 : TT::row(64 + (int)li);
     const uint32_t tabl = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)tabb;  // LDS address
 
     // V lives in [2^23, 2^24), where the fp32 ulp is 1 and the low mantissa bits ARE the low integer
@@ -765,7 +731,7 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(8))
         fscale = (1u << 20) / (tot ? tot : 1u);
     }
     const uint64_t availB = IN::bytes(geo.availStages);
-    const uint32_t vo1 = IN::voff(sA), vo2 = LR ? IN::voff(sB) : IN::voff((int)li);
+    const uint32_t vo1 = IN::voff(sA), vo2 = IN::voff(sB);
     // segment workgroups (uniform bookkeeping): bit q of `verified` = segment q checked exact (segments
     // that start at a chunk start are exact).  vS / vE: this segment's start / end vector; vIn: the vector a
     // re-decode starts from (left neighbour's end vector).
@@ -797,7 +763,7 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(8))
     uint32_t tbn = pass == 0 ? LL::TBS - 3 * (blockIdx.x & 3) : LL::TBS;
     __amdgpu_buffer_rsrc_t rs = tg_rsrc<CH>(in, start + 32ull * j0, availB);
     typename IN::raw_t rA = IN::template load<0>(rs, vo1);               // stage sA of the group
-    typename IN::raw_t rB = IN::template load<LR ? 0 : 2>(rs, vo2);      // stage sB
+    typename IN::raw_t rB = IN::template load<0>(rs, vo2);               // stage sB
 
     // Branch-metric table reads, software-pipelined: the entries of stage r are loaded TGD stages
     // ahead; one ds_read_b64 at an even period also carries the entry of the stage 6 later.  The
@@ -805,15 +771,12 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(8))
     // program order -- left alone the compiler merges neighbours into ds_read2_b64 (8 cycles).
     constexpr int TGD = 4;  // 6 or 8 measured the same (profiles/r02/ablate_prefetch.log)
     typedef __attribute__((address_space(3))) const volatile f2v* lptr;
-    typedef __attribute__((address_space(3))) const volatile float* lptr1;
     const __attribute__((address_space(3))) char* tl = (const __attribute__((address_space(3))) char*)tabb;
-    f2v vp[96];  // entry pair read for stage r (even period of a pair, or every INT phase-0 stage)
+    f2v vp[96];  // entry pair read for stage r (the even period of a period pair)
     auto issue = [&](auto Rc) {
         constexpr int r = decltype(Rc)::value;  // stage within the group (the group starts at phase 0)
         constexpr int K = r % 6;
         if constexpr (ABL & kAblNoTabReads) {
-        } else if constexpr (TT::pairrow(K)) {  // INT phase 0: this lane's tag sign only
-            vp[r] = (f2v){*(lptr1)(tl + aU0 + TT::row(r)), 0.0f};
         } else if constexpr ((r / 6) % 2 == 0) {
             vp[r] = *(lptr)(tl + aK[K] + TT::row(r));
         }
@@ -828,9 +791,9 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(8))
             constexpr int Q = (K + 5) % 6;
             constexpr int r = 32 * BB + i;  // stage within the group
             constexpr bool ODD = (r / 6) % 2 == 1;
-            constexpr int RP = TT::pairrow(K) ? r : (ODD ? r - 6 : r);  // where this stage's pair was read
+            constexpr int RP = ODD ? r - 6 : r;  // where this stage's pair was read
             const f2v e = (ABL & kAblNoTabReads) ? (f2v){(float)aK[K], 1.0f} : vp[RP];
-            const float m = TT::pairrow(K) || !ODD ? e.x : e.y;
+            const float m = ODD ? e.y : e.x;
             // Q = 0..3: DPP stage (lane xor 1, 2, 7, 8); Q = 4: xor 16 through ds_swizzle; Q = 5: xor 32
             // through ds_bpermute
             if constexpr (INT) {
@@ -894,8 +857,7 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(8))
                 // multiple of 3 (batches of TBS - 3 (blockIdx.x & 3) or TBS words), so word k's phase follows
                 // from the lane; otherwise (SOFT16: 11) from k.  The M_B32 kernels have no VGPR to keep the
                 // lane's constants in (64 at 8 waves per SIMD) and compute them here.
-                const TbC tc = LL::TBS % 3 == 0 && CORE != B32 && !(ABL & kAblTbPerWord) ? tb_unpack<CORE == B32>(tbk)
-                                                                                          : tb_direct<J, CORE == B32>((int)k);
+                const TbC tc = LL::TBS % 3 == 0 && CORE != B32 ? tb_unpack<CORE == B32>(tbk) : tb_direct<J, CORE == B32>((int)k);
                 uint32_t w = traceback_word_tg<J, CORE == B32>((const char*)ring, (uint32_t)(lane + 1) * 256u, tc);
                 if constexpr (OB == 32) {
                     ((uint32_t*)out)[wOut + k] = w;
@@ -913,73 +875,41 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(8))
         }
         return j + 1 < nblk;
     };
-    // table row of stage phase K from the stage's (A, B) = (BM[3], BM[2]): E[L] = BM[L]*2^S + tag at
-    // entries 0, 2, 4, 6 (the odd dwords are the other period's); INT phase-0 rows: the pairs (E-[L], E+[L])
-    // part 0: the entries of stage sA (all lanes), part 1: of stage sB (lanes 0..31)
+    // the four entries of a stage from its (A, B) = (BM[3], BM[2]): E[L] = BM[L]*2^S + tag, one per label
+    // region (INT phase-0 stages also the +tag entries of the ALT area); part 0: the entries of stage sA
+    // (all lanes), part 1: of stage sB (lanes 0..31)
     auto put_row = [&](auto PT, auto A, auto B, int K) {  // A, B: ints, or floats (IN::FAB)
         constexpr int part = decltype(PT)::value;
-        const int rb = part ? rowb2 : rowb1;
         const float tg0 = part ? tg0B : tg0A;
         if constexpr (INT) {
-            uint32_t* e = (uint32_t*)(tabb + rb);
-            // the tag of the row's own class: -2^j (the int32 core: exchanged wins ties)
+            // the tag of the entry's own class: -2^j (the int32 core: exchanged wins ties)
             const int a = A * (1 << S), b = B * (1 << S), tag = -(int)tg0;
-            if constexpr (LR) {
-                auto f = [](int x) { return __builtin_bit_cast(float, x); };
-                lds_write_addtid4<256 * part, TT::REGION>(tabl, f(-a - tag), f(-b - tag), f(b - tag), f(a - tag));
-                if (K == 0)  // phase-0 lanes: the +tag entries (ALT), at dword ALT + index + 2L
-                    lds_write_addtid4<TT::ALT_OFF + 256 * part, 8>(tabl, f(-a + tag), f(-b + tag), f(b + tag), f(a + tag));
-                return;
-            }
-            e[0] = (uint32_t)(-a - tag);
-            e[2] = (uint32_t)(-b - tag);
-            e[4] = (uint32_t)(b - tag);
-            e[6] = (uint32_t)(a - tag);
-            if (K == 0) {
-                e[1] = (uint32_t)(-a + tag);
-                e[3] = (uint32_t)(-b + tag);
-                e[5] = (uint32_t)(b + tag);
-                e[7] = (uint32_t)(a + tag);
-            }
+            auto f = [](int x) { return __builtin_bit_cast(float, x); };
+            lds_write_addtid4<256 * part, TT::REGION>(tabl, f(-a - tag), f(-b - tag), f(b - tag), f(a - tag));
+            if (K == 0)  // phase-0 lanes: the +tag entries (ALT), at dword ALT + index + 2L
+                lds_write_addtid4<TT::ALT_OFF + 256 * part, 8>(tabl, f(-a + tag), f(-b + tag), f(b + tag), f(a + tag));
             return;
         }
         constexpr float SC = (float)(1 << S);
         const float af = (float)A, bf = (float)B;
-        float* e = (float*)(tabb + rb);
         const float E0 = __builtin_fmaf(af, -SC, tg0), E1 = __builtin_fmaf(bf, -SC, tg0);
         const float E2 = __builtin_fmaf(bf, SC, tg0), E3 = __builtin_fmaf(af, SC, tg0);
-        if constexpr (ABL & kAblNoTabWrites) {  // tools only: compute the row, do not store it
+        if constexpr (ABL & kAblNoTabWrites) {  // tools only: compute the entries, do not store them
             asm volatile("" ::"v"(E0), "v"(E1), "v"(E2), "v"(E3));
             return;
         }
-        if constexpr (LR) {
-            lds_write_addtid4<256 * part, TgTabL::REGION>(tabl, E0, E1, E2, E3);
-            return;
-        }
-        e[0] = E0;
-        e[2] = E1;
-        e[4] = E2;
-        e[6] = E3;
+        lds_write_addtid4<256 * part, TgTabL::REGION>(tabl, E0, E1, E2, E3);
     };
-    // S01: rows from the two soft values (six FMAs) instead of (A, B) = (s0 + s1, s0 - s1) (two integer
+    // S01: entries from the two soft values (six FMAs) instead of (A, B) = (s0 + s1, s0 - s1) (two integer
     // ops, two converts, four FMAs); fp32 cores
     constexpr bool S01 = HasS01<IN>::value && !INT;
     auto put_row_s01 = [&](auto PT, float s0, float s1) {
         constexpr int part = decltype(PT)::value;
-        const int rb = part ? rowb2 : rowb1;
         const float tg0 = part ? tg0B : tg0A;
         constexpr float SC = (float)(1 << S);
         const float X = __builtin_fmaf(s0, SC, tg0), Y = __builtin_fmaf(s0, -SC, tg0);
-        if constexpr (LR) {
-            lds_write_addtid4<256 * part, TgTabL::REGION>(tabl, __builtin_fmaf(s1, -SC, Y), __builtin_fmaf(s1, SC, Y),
-                                                          __builtin_fmaf(s1, -SC, X), __builtin_fmaf(s1, SC, X));
-            return;
-        }
-        float* e = (float*)(tabb + rb);
-        e[0] = __builtin_fmaf(s1, -SC, Y);
-        e[2] = __builtin_fmaf(s1, SC, Y);
-        e[4] = __builtin_fmaf(s1, -SC, X);
-        e[6] = __builtin_fmaf(s1, SC, X);
+        lds_write_addtid4<256 * part, TgTabL::REGION>(tabl, __builtin_fmaf(s1, -SC, Y), __builtin_fmaf(s1, SC, Y),
+                                                      __builtin_fmaf(s1, -SC, X), __builtin_fmaf(s1, SC, X));
     };
     const int r6a = sA % 6, r6b = sB % 6;
     using P0 = std::integral_constant<int, 0>;
@@ -1012,7 +942,7 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(8))
         if constexpr (!(ABL & kAblNoLoads)) {
             rs = tg_rsrc<CH>(in, start + 32ull * (j + 3), availB);
             rA = IN::template load<0>(rs, vo1);
-            rB = IN::template load<LR ? 0 : 2>(rs, vo2);
+            rB = IN::template load<0>(rs, vo2);
         }
         // every other group head (6 blocks): 0.7 % faster than every head, every third is 1 % slower
         // (profiles/r02/benchab_fair.log)
