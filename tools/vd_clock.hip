@@ -16,7 +16,7 @@
 #include "../gpu-accelerated-viterbi-decoder_amd/csrc/vd_kernel_tg.h"
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP error %s at %d\n", hipGetErrorString(e), __LINE__); exit(1); } } while (0)
 using KFn = void (*)(const void*, void*, vd::Geom);
-struct Variant { const char* name; KFn fn; bool soft; };
+struct Variant { const char* name; KFn fn; int in; };  // in: 0 HARD, 1 SOFT8, 2 FP32
 
 int main(int argc, char** argv)
 {
@@ -44,16 +44,30 @@ int main(int argc, char** argv)
         const uint32_t s0 = q8((o0[t] ? -1.0 : 1.0) + G(rng)), s1 = q8((o1[t] ? -1.0 : 1.0) + G(rng));
         hs[t / 2] |= ((s0 << 8) | s1) << (16 * ((t % 2) ^ 1));
     }
+    // FP32: the same noisy BPSK values as floats scaled like the packer's FP32 path (x 40000 / 2^13 here:
+    // the kernel clamps to [-8, 7]), two per stage
+    std::vector<float> hf(2 * N + 128, 0.0f);
+    {
+        std::mt19937 r2(11);
+        std::normal_distribution<double> G2(0.0, sigma);
+        for (size_t t = 0; t < N; t++) {
+            hf[2 * t] = (float)(((o0[t] ? -1.0 : 1.0) + G2(r2)) * 4.0);
+            hf[2 * t + 1] = (float)(((o1[t] ? -1.0 : 1.0) + G2(r2)) * 4.0);
+        }
+    }
     const size_t strH = (hh.size() * 4 + 255) / 256 * 256, strS = (hs.size() * 4 + 255) / 256 * 256;
-    void *bH, *bS, *out;
+    const size_t strF = (hf.size() * 4 + 255) / 256 * 256;
+    void *bH, *bS, *bF, *out;
     CK(hipMalloc(&bH, strH * steps));
     CK(hipMalloc(&bS, strS * steps));
+    CK(hipMalloc(&bF, strF * steps));
     // outputs at stride 0 (timing only): the clock stamps sit at out + 16 MiB + 48 B per launch wave
     const size_t outBytes = (16u << 20) + (size_t)6400 * steps * 48;
     CK(hipMalloc(&out, outBytes));
     for (int k = 0; k < steps; k++) {
         CK(hipMemcpy((char*)bH + k * strH, hh.data(), hh.size() * 4, hipMemcpyHostToDevice));
         CK(hipMemcpy((char*)bS + k * strS, hs.data(), hs.size() * 4, hipMemcpyHostToDevice));
+        CK(hipMemcpy((char*)bF + k * strF, hf.data(), hf.size() * 4, hipMemcpyHostToDevice));
     }
     vd::Geom g;
     g.packNum = (N - 64) / 32;
@@ -66,14 +80,16 @@ int main(int argc, char** argv)
     CK(hipMemset(g.fair, 0xFF, vd::kFairBoardWords * 4));
     constexpr int C = vd::kAblClock;
     const Variant vs[] = {
-        {"hard  full", (KFn)vd::vd_decode_tg<vd::HARD, vd::B32, 32, C>, false},
-        {"hard  ACS only", (KFn)vd::vd_decode_tg<vd::HARD, vd::B32, 32, C | vd::kAblAcsOnly>, false},
-        {"hard  -tabreads", (KFn)vd::vd_decode_tg<vd::HARD, vd::B32, 32, C | vd::kAblNoTabReads>, false},
-        {"hard  -traceback", (KFn)vd::vd_decode_tg<vd::HARD, vd::B32, 32, C | vd::kAblNoTraceback>, false},
-        {"hard  -tabbuild", (KFn)vd::vd_decode_tg<vd::HARD, vd::B32, 32, C | vd::kAblNoTabBuild>, false},
-        {"soft8 full", (KFn)vd::vd_decode_tg<vd::SOFT8, vd::B16, 32, C>, true},
-        {"soft8 ACS only", (KFn)vd::vd_decode_tg<vd::SOFT8, vd::B16, 32, C | vd::kAblAcsOnly>, true},
-        {"soft8 -tabreads", (KFn)vd::vd_decode_tg<vd::SOFT8, vd::B16, 32, C | vd::kAblNoTabReads>, true},
+        {"hard  full", (KFn)vd::vd_decode_tg<vd::HARD, vd::B32, 32, C>, 0},
+        {"hard  ACS only", (KFn)vd::vd_decode_tg<vd::HARD, vd::B32, 32, C | vd::kAblAcsOnly>, 0},
+        {"hard  -tabreads", (KFn)vd::vd_decode_tg<vd::HARD, vd::B32, 32, C | vd::kAblNoTabReads>, 0},
+        {"hard  -traceback", (KFn)vd::vd_decode_tg<vd::HARD, vd::B32, 32, C | vd::kAblNoTraceback>, 0},
+        {"hard  -tabbuild", (KFn)vd::vd_decode_tg<vd::HARD, vd::B32, 32, C | vd::kAblNoTabBuild>, 0},
+        {"soft8 full", (KFn)vd::vd_decode_tg<vd::SOFT8, vd::B16, 32, C>, 1},
+        {"soft8 ACS only", (KFn)vd::vd_decode_tg<vd::SOFT8, vd::B16, 32, C | vd::kAblAcsOnly>, 1},
+        {"soft8 -tabreads", (KFn)vd::vd_decode_tg<vd::SOFT8, vd::B16, 32, C | vd::kAblNoTabReads>, 1},
+        {"fp32  full", (KFn)vd::vd_decode_tg<vd::FP32, vd::F16, 32, C>, 2},
+        {"fp32  ACS only", (KFn)vd::vd_decode_tg<vd::FP32, vd::F16, 32, C | vd::kAblAcsOnly>, 2},
     };
     const int nv = sizeof(vs) / sizeof(vs[0]);
     const unsigned grid = 1600u * (unsigned)steps;
@@ -86,8 +102,8 @@ int main(int argc, char** argv)
     CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
     auto launch = [&](const Variant& v) {
         vd::Geom gg = g;
-        gg.inStride = v.soft ? strS : strH;
-        hipLaunchKernelGGL(v.fn, dim3(grid), dim3(256), 0, 0, v.soft ? bS : bH, out, gg);
+        gg.inStride = v.in == 2 ? strF : v.in == 1 ? strS : strH;
+        hipLaunchKernelGGL(v.fn, dim3(grid), dim3(256), 0, 0, v.in == 2 ? bF : v.in == 1 ? bS : bH, out, gg);
     };
     // warm-up: 0.5 s of launches (the clock ramps from idle)
     {
