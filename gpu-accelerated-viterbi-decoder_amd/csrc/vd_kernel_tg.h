@@ -116,8 +116,8 @@ __device__ __forceinline__ void lds_write_addtid4(uint32_t base, float v0, float
 // Survivor ring: as many 256-B slots as fit next to the table in a wave's 5,120 B (8 workgroups of 4 waves
 // per CU, so every SIMD holds 8 waves at <= 64 VGPRs); one traceback batch traces (slots - 1) words, and
 // its VALU instructions cost the same whatever the number of words, so the longest ring is the cheapest:
-// 13 slots with the fp32 cores' label-region table (1,664 B), 12 with SOFT16's (1,936 B).  8 waves beat 7 with a longer ring by 1.4 % per batch
-// (profiles/r02/benchab_8w.log).
+// 13 slots with the fp32 cores' label-region table (1,664 B), 12 with SOFT16's (1,936 B).  8 waves beat 7
+// with a longer ring by 1.4 % per batch (profiles/r02/benchab_8w.log).
 constexpr int kGuardWords = 4;                 // guard words before the table, between table and ring, after the ring
 constexpr uint32_t kGuardPattern = 0xA5C3E10Fu;
 constexpr int kWaveLdsWords = 163840 / 4 / (8 * kWaves);  // 1,280: a wave's share at 8 workgroups per CU
