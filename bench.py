@@ -3,8 +3,9 @@
 
 One step = one pass of the decode hot path over one batch of each headline workload, inputs
 already resident in HBM:
-  * HARD  input, int32 metric core   (BASELINE configs[1]: 32M bits, `-i h -m b32`)
-  * SOFT8 input, int16x2 metric core (BASELINE configs[2]: 32M bits, `-i s8 -m b16`)
+  * HARD  input, M_B32 option       (BASELINE configs[1]: 32M bits, `-i h -m b32`)
+  * SOFT8 input, M_B16 option       (BASELINE configs[2]: 32M bits, `-i s8 -m b16`)
+both on the fp32 exact-integer tagged core, which reproduces each option's tie rule.
 value = decoded bits of both batches (2 x getMessageLen(64e6) = 63,999,872) / step time, summed
 over ranks.  Multi-GPU (BASELINE configs[3]): one process per GPU, each rank decodes its own
 independent batches (weak scaling, no data-path collective; an RCCL all_gather of per-rank
@@ -93,6 +94,32 @@ def cpu_baseline(batches):
             "sample": f"one full bench step ({names}, 2 x 32M-bit batches, 6400-chunk partition) decoded by "
                       f"oracle/vd_oracle.c on 1 host thread in {dt:.1f} s; output identical to the GPU's: {match}",
             "matches_gpu": match, "all_cores": all_cores}
+
+
+def parity_block(checks):
+    """Word-for-word check of GPU outputs against the oracle (oracle/vd_oracle.c, the checker) on the host
+    threads of this job, after the timed region: per path, the words compared and the mismatches.  checks:
+    (path, options, packed input or float channel values, GPU output bytes, inputNum, packer scale or None
+    -- with a scale the oracle packs the floats itself, SoftDecisionPacker restated, before decoding)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import vd_oracle as vo
+    nt = max(1, min(16, len(os.sched_getaffinity(0))))
+    res = {}
+    t0 = time.perf_counter()
+    for path, opt, inp, gout, n, scale in checks:
+        packed = vo.pack(opt, inp.view(np.float32), scale) if scale is not None else inp.view(vo.in_dtype(opt))
+        ref, ok = vo.decode(opt, packed, input_num=n, nthreads=nt)
+        got = gout.view(np.uint8)[:ref.nbytes].view(ref.dtype)
+        mism = int(np.count_nonzero(ref != got)) if got.size == ref.size else -1
+        res[path] = {"options": hex(opt), "words": int(ref.size), "mismatches": mism}
+    bad = [k for k, v in res.items() if v["mismatches"] != 0]
+    return {"what": "GPU output vs oracle/vd_oracle.c (the CPU restatement) word for word, after the timed region: "
+                    "both headline workloads (batch 0, and the last batch of the launch, whose waves run the "
+                    "fairness controller), the other formats/cores (BASELINE configs[4] FP32/f16, SOFT4, SOFT16, "
+                    "16-bit output words), the single-batch segment launches, and the fused float-input decode "
+                    "(oracle: SoftDecisionPacker restated, then decode)",
+            "paths": res, "all_match": not bad, "mismatching_paths": bad,
+            "host_threads": nt, "seconds": round(time.perf_counter() - t0, 2)}
 
 
 def cpu_model():
@@ -342,10 +369,11 @@ def settle(fn, seconds=0.3):
     torch.cuda.synchronize()
 
 
-def other_configs_side_measurement(dev, sptr, stream, reps=20):
+def other_configs_side_measurement(dev, sptr, stream, reps=20, keep=None):
     """Kernel-only Gb/s of the other input formats / cores at 32M bits (BASELINE configs[4] = FP32 input
     on the fp16 core, plus SOFT4, SOFT16 and 16-bit output words), inputs synthesised by the GPU channel
-    source at the bench SNR.  Outside the timed region; never `value`."""
+    source at the bench SNR.  Outside the timed region; never `value`.  keep: a list that receives host
+    copies (input, output) of batch 0 and of the launch's last batch for the parity block."""
     res = {}
     for i, (name, opt) in enumerate(OTHER_CONFIGS):
         n = 2 * N_BITS
@@ -369,21 +397,28 @@ def other_configs_side_measurement(dev, sptr, stream, reps=20):
         ber = max(batch_ber(opt, bits, outs, ostride, nout, k, msg)[0] for k in (0, reps - 1))
         res[name] = {"kernel": vitdec.kernel_name(opt), "kernel_ms": round(ms, 4),
                      "gbps": round(msg / (ms * 1e-3) / 1e9, 2), "ber": ber, "batches_per_launch": reps}
+        if keep is not None:  # host copies for the parity block: batch 0 and the last batch of the launch
+            nin = vitdec.lib().vd_input_size(opt, n)
+            for k in (0, reps - 1):
+                keep.append((f"other_configs.{name}[batch {k}]", opt, inps[k * istride:k * istride + nin].cpu().numpy(),
+                             outs[k * ostride:k * ostride + nout].cpu().numpy(), n, None))
         dec.close()
         del inps, bits, outs
     return res
 
 
-def single_launch_side_measurement(batches, stream, sptr, reps=20):
+def single_launch_side_measurement(batches, stream, sptr, reps=20, keep=None):
     """The reference run()'s unit of work on device buffers: one vd_run_device launch per 32M-bit batch
-    (split launch, 6400-chunk partition), `reps` of the bench's resident batches back to back, per batch
-    = time / reps.  Outside the timed region; never `value` (the timed region batches its launches)."""
+    (segment launch, 6400-chunk partition), `reps` of the bench's resident batches back to back, per batch
+    = time / reps, into buffers of their own.  Outside the timed region; never `value` (the timed region
+    batches its launches).  keep: receives batch 0's segment-launch output for the parity block."""
     res = {}
     for b in batches:
         K = b["outs"].numel() // b["ostride"]
         n = min(reps, K)
+        souts = torch.empty(n * b["ostride"], dtype=torch.uint8, device=b["outs"].device)
         run = lambda: [b["dec"].run_device(b["inps"].data_ptr() + k * b["istride"],
-                                           b["outs"].data_ptr() + k * b["ostride"], b["input_num"], sptr)
+                                           souts.data_ptr() + k * b["ostride"], b["input_num"], sptr)
                        for k in range(n)]
         settle(run)
         e = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
@@ -392,11 +427,21 @@ def single_launch_side_measurement(batches, stream, sptr, reps=20):
         e[1].record(stream)
         torch.cuda.synchronize()
         ms = e[0].elapsed_time(e[1]) / n
-        res[b["name"]] = {"kernel_ms": round(ms, 4), "gbps": round(b["msg"] / (ms * 1e-3) / 1e9, 2), "launches": n}
+        nout = b["nout"]
+        # every segment-launch output equals the batched launch's output of the same batch (word for word,
+        # on the GPU); batch 0 also goes to the oracle in the parity block
+        same = [bool(torch.equal(souts[k * b["ostride"]:k * b["ostride"] + nout], b["outs"][k * b["ostride"]:k * b["ostride"] + nout]))
+                for k in range(n)]
+        res[b["name"]] = {"kernel_ms": round(ms, 4), "gbps": round(b["msg"] / (ms * 1e-3) / 1e9, 2), "launches": n,
+                          "equals_batched_launch": f"{sum(same)} of {n} batches"}
+        if keep is not None:
+            keep.append((f"single_launch.{b['name']}[batch 0]", b["opt"], b["inp"].cpu().numpy(),
+                         souts[:nout].cpu().numpy(), b["input_num"], None))
+        del souts
     return res
 
 
-def llr_side_measurement(dev, sptr, stream, reps=20):
+def llr_side_measurement(dev, sptr, stream, reps=20, keep=None):
     """Float channel values in HBM (the reference's AddNoise output, before SoftDecisionPacker): the GPU
     packer alone, packer + decode, and the fused decode (quantisation in the table build), SOFT8/int16.
     Outside the timed region; not part of `value`."""
@@ -448,6 +493,10 @@ def llr_side_measurement(dev, sptr, stream, reps=20):
     torch.cuda.synchronize()
     t_batched = e[0].elapsed_time(e[1]) / reps
     same_b = bool(torch.equal(outs[:nout], out_fused))
+    if keep is not None:  # the oracle packs the same floats (SoftDecisionPacker restated) and decodes them
+        keep.append(("llr_input.fused_single", opt, vals.cpu().numpy(), out_fused.cpu().numpy(), n, 40000.0))
+        keep.append((f"llr_input.fused_batched[batch {reps - 1}]", opt, many[(reps - 1) * n:reps * n].cpu().numpy(),
+                     outs[(reps - 1) * ostride:(reps - 1) * ostride + nout].cpu().numpy(), n, 40000.0))
     dec.close()
     del many, outs
     return {"workload": "64M float32 channel values (32M-bit SOFT8 batch, scale 40000) resident in HBM",
@@ -549,6 +598,7 @@ def main():
     ap.add_argument("--no-pcie", action="store_true", help="skip the host-to-host pipelined side measurement")
     ap.add_argument("--no-channel", action="store_true", help="skip the channel-source side measurement")
     ap.add_argument("--no-other", action="store_true", help="skip the other-formats side measurement")
+    ap.add_argument("--no-parity", action="store_true", help="skip the oracle parity block (profiling runs)")
     ap.add_argument("--workloads", default=DEFAULT_WORKLOADS,
                     help="profiling runs only: comma-separated workloads to time (" + ",".join(ALL_WORKLOADS) + ")")
     ap.add_argument("--ranks-check", action="store_true", help=argparse.SUPPRESS)  # tests: rank layout only
@@ -686,9 +736,19 @@ def main():
     # the other formats and the fused float input run in launches of as many batches as the timed region's
     # (at least 20): a shorter launch carries more of the once-per-launch ramp and tail per batch
     side_reps = max(20, P)
-    other = None if (args.no_other or not side) else other_configs_side_measurement(dev, sptr, stream, side_reps)
-    single = None if (args.no_other or not side) else single_launch_side_measurement(batches, stream, sptr)
-    llr = None if (args.no_llr or not side) else llr_side_measurement(dev, sptr, stream, side_reps)
+    # parity block (rank 0, every N): host copies of the outputs to check against the oracle at the end
+    checks = [] if (rank == 0 and not args.no_parity) else None
+    if checks is not None:
+        for b in batches:
+            for k in sorted({0, P - 1}):
+                nin = b["inp"].numel()
+                checks.append((f"{b['name']}[batch {k}]", b["opt"],
+                               b["inps"][k * b["istride"]:k * b["istride"] + nin].cpu().numpy(),
+                               b["outs"][k * b["ostride"]:k * b["ostride"] + b["nout"]].cpu().numpy(), b["input_num"],
+                               40000.0 if b["llr"] else None))
+    other = None if (args.no_other or not side) else other_configs_side_measurement(dev, sptr, stream, side_reps, checks)
+    single = None if (args.no_other or not side) else single_launch_side_measurement(batches, stream, sptr, keep=checks)
+    llr = None if (args.no_llr or not side) else llr_side_measurement(dev, sptr, stream, side_reps, checks)
     chan = None if (args.no_channel or not side) else channel_side_measurement(dev, sptr)
     pcie = None if (args.no_pcie or not side) else pcie_side_measurement(batches, dev)
     # the same collectives at every N (N = 1: a 1-rank RCCL group)
@@ -748,9 +808,10 @@ def main():
                     f"bits, K=7 (0171,0133) encoder, BPSK + normal_distribution<float> AWGN at {SNR_DB} dB, "
                     f"quantiser scale 40000), seeds (1+2i, 2+2i) for batch i = 2 rank + workload",
             "config": {
-                "workload": "per GPU per step: one 32M-bit HARD batch on the int32 core + one 32M-bit SOFT8 "
-                            "batch on the int16x2 core (BASELINE configs[1]+[2]); each batch uses the "
-                            "reference's 6400-chunk partition",
+                "workload": "per GPU per step: one 32M-bit HARD batch with the M_B32 option (int32 tie rule) + "
+                            "one 32M-bit SOFT8 batch with the M_B16 option (int16 tie rule), BASELINE configs[1]+[2], "
+                            "both on the fp32 exact-integer tagged core (not a V_PK int16x2 core: DESIGN.md 4 "
+                            "'Packed int16'); each batch uses the reference's 6400-chunk partition",
                 "n_bits_per_batch": N_BITS,
                 "decoded_bits_per_batch": batches[0]["msg"],
                 "parallelism": f"batch-shard x{world}" if world > 1 else "single GPU (1-rank RCCL group)",
@@ -811,7 +872,9 @@ def main():
             result["config"]["final_gather"] = final_gather
         if not metric_run:
             result["config"]["profiling_workloads"] = names
-        if not args.no_cpu_baseline and world == 1 and metric_run:
+        if checks is not None:
+            result["config"]["parity"] = parity_block(checks)
+        if not args.no_cpu_baseline and metric_run:  # every N, on rank 0 (the node's own cores)
             result["cpu_baseline"] = cpu_baseline(batches)
         print(json.dumps(result), flush=True)
 

@@ -136,14 +136,19 @@ launch_fn pick(int o, bool llr)
     return llr ? pick_ch<vd::kLlr>(o) : pick_ch<0>(o);
 }
 
+// CORE names the option's tie rule; every kernel computes on the fp32 exact-integer tagged core (SOFT16:
+// int32 patterns), none on packed int16 / fp16 arithmetic
 const char* kname(int o)
 {
     static const char* names[5][3] = {
-        {"vd_decode_tg<HARD,B32>", "vd_decode_tg<HARD,B16>", "vd_decode_tg<HARD,F16>"},
-        {"vd_decode_tg<SOFT4,B32>", "vd_decode_tg<SOFT4,B16>", "vd_decode_tg<SOFT4,F16>"},
-        {"vd_decode_tg<SOFT8,B32>", "vd_decode_tg<SOFT8,B16>", "-"},
-        {"vd_decode_tg<SOFT16,B32> (int32 patterns)", "-", "-"},
-        {"vd_decode_tg<FP32,B32>", "vd_decode_tg<FP32,B16>", "vd_decode_tg<FP32,F16>"},
+        {"vd_decode_tg<HARD,B32> (fp32 tagged core, M_B32 tie rule)", "vd_decode_tg<HARD,B16> (fp32 tagged core, M_B16 tie rule)",
+         "vd_decode_tg<HARD,F16> (fp32 tagged core, M_FP16 tie rule)"},
+        {"vd_decode_tg<SOFT4,B32> (fp32 tagged core, M_B32 tie rule)", "vd_decode_tg<SOFT4,B16> (fp32 tagged core, M_B16 tie rule)",
+         "vd_decode_tg<SOFT4,F16> (fp32 tagged core, M_FP16 tie rule)"},
+        {"vd_decode_tg<SOFT8,B32> (fp32 tagged core, M_B32 tie rule)", "vd_decode_tg<SOFT8,B16> (fp32 tagged core, M_B16 tie rule)", "-"},
+        {"vd_decode_tg<SOFT16,B32> (int32 tagged patterns, M_B32 tie rule)", "-", "-"},
+        {"vd_decode_tg<FP32,B32> (fp32 tagged core, M_B32 tie rule)", "vd_decode_tg<FP32,B16> (fp32 tagged core, M_B16 tie rule)",
+         "vd_decode_tg<FP32,F16> (fp32 tagged core, M_FP16 tie rule)"},
     };
     if (!valid(o)) return "-";
     return names[ch_of(o)][met_of(o)];
@@ -426,7 +431,10 @@ int vd_set_guard_check(vd_decoder* d, int enable)
         d->check = nullptr;
         return VD_OK;
     }
-    if (!d->check) VD_HIP(hipMalloc(&d->check, 4));
+    // kernels still in flight on the decoder's or a caller's (non-blocking) stream may add to the counter:
+    // let them finish before the reset
+    if (d->check) VD_HIP(hipDeviceSynchronize());
+    else VD_HIP(hipMalloc(&d->check, 4));
     VD_HIP(hipMemset(d->check, 0, 4));
     VD_HIP(hipDeviceSynchronize());
     return VD_OK;
@@ -459,6 +467,9 @@ int vd_run_device_batch(vd_decoder* d, const void* input_d, size_t input_stride,
     if (message_len(d->options, inputNum) == 0) return fail(VD_ERR_ARG, "inputNum too small");
     if (nbatch > 1 && output_stride < message_len(d->options, inputNum) / 8)
         return fail(VD_ERR_ARG, "output_stride smaller than the output size: batches would overlap");
+    // input_stride 0 = every batch decodes the same input (broadcast); otherwise the inputs may not overlap
+    if (nbatch > 1 && input_stride != 0 && input_stride < input_size(d->options, inputNum))
+        return fail(VD_ERR_ARG, "input_stride smaller than the input size: batches would overlap");
     if ((uint64_t)vd::kChunks * (uint64_t)nbatch > 0xFFFFFFFFull) return fail(VD_ERR_ARG, "nbatch too large");
     if ((input_stride | output_stride) & 3) return fail(VD_ERR_ARG, "strides must be multiples of 4 bytes");
     if (nbatch == 1) return launch_decode(d, input_d, output_d, inputNum, (hipStream_t)stream);

@@ -14,8 +14,9 @@ namespace vd {
 //  thirds: 8 workgroups per CU, each 3 chunks in 4 segments of 3/4 chunk, except one workgroup per CU of 4
 //          chunks (segments of 1 chunk): 8 waves per SIMD for the whole launch.  Workgroups go to the 8
 //          XCDs round robin (workgroup g to XCD g % 8, its n = g / 8-th there); the 4-chunk ones are those
-//          with n / 32 == (n % 32) % 8, one in every 32 consecutive n and one in every aligned 8: one per
-//          CU whether the XCD deals its 256 workgroups to its 32 CUs round robin or 8 at a time.
+//          with n / 32 == (n % 32) % 8: four in every aligned 32 consecutive n (one per aligned 8) and one
+//          per residue class of n mod 32, so one per CU whether the XCD deals its 256 workgroups to its 32
+//          CUs round robin (CU = n % 32) or 8 at a time (CU = n / 8); tests/cxx/segplan_check.cpp checks both.
 inline std::vector<uint32_t> seg_table(int nsimd, bool thirds)
 {
     std::vector<uint32_t> t{0u};

@@ -45,7 +45,7 @@ EXPORTS = ["vd_options_valid", "vd_input_size", "vd_message_len", "vd_output_siz
            "vd_simulate_host", "vd_count_errors", "vd_last_error", "vd_device_count", "vd_kernel_name",
            "vd_pack_device", "vd_run_device_llr", "vd_run_llr", "vd_host_alloc", "vd_host_free",
            "vd_run_stream", "vd_channel_device", "vd_simulate_device", "vd_mt_state_after", "vd_split_redecodes",
-           "vd_set_guard_check", "vd_guard_violations", "vd_run_device_llr_batch"]
+           "vd_set_guard_check", "vd_guard_violations", "vd_run_device_llr_batch", "vd_build_info"]
 
 
 class VitdecError(RuntimeError):
@@ -63,6 +63,11 @@ def lib():
     if not os.path.exists(LIB_PATH):
         raise VitdecError(f"{LIB_PATH} not built: run `make -C {_HERE}` (or __graft_entry__.build())")
     L = ctypes.CDLL(LIB_PATH)
+    if not os.environ.get("VITDEC_LIB"):  # the product library must be built from the sources in this tree
+        L.vd_build_info.restype = ctypes.c_char_p
+        stale = build_mismatch(L.vd_build_info().decode())
+        if stale:
+            raise VitdecError(f"{LIB_PATH} is stale ({stale}): rebuild it with `make -C {_HERE}`")
     sz, vp, i, f = ctypes.c_size_t, ctypes.c_void_p, ctypes.c_int, ctypes.c_float
     L.vd_options_valid.argtypes = [i]
     for n in ("vd_input_size", "vd_message_len", "vd_output_size"):
@@ -97,6 +102,22 @@ def lib():
     L.vd_kernel_name.restype = ctypes.c_char_p
     _lib = L
     return L
+
+
+def build_mismatch(info):
+    """None when the sources named in the library's build record hash to the recorded value, else why not."""
+    import hashlib
+    parts = info.split()
+    if len(parts) < 2:
+        return "no build record"
+    h = hashlib.sha256()
+    for rel in parts[1:]:
+        p = os.path.join(_HERE, rel)
+        if not os.path.exists(p):
+            return f"source {rel} missing"
+        with open(p, "rb") as fh:
+            h.update(fh.read())
+    return None if h.hexdigest()[:16] == parts[0] else "sources changed since the build"
 
 
 def _check(rc):

@@ -12,4 +12,4 @@ timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.
 timeout -k 10 400 python bench.py > $O/bench.log 2> $O/bench.err
 echo rc=$?
 cat $O/smoke.log
-tail -1 $O/bench.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); c=d['config']; print(d['value'], d['ms_per_step'], c['kernel_ms'], c['ber'], {k: v['gbps'] for k, v in c['other_configs'].items()}, c['single_launch'], c['final_gather'], d['cpu_baseline']['matches_gpu'])"
+tail -1 $O/bench.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); c=d['config']; print(d['value'], d['ms_per_step'], c['kernel_ms'], c['ber'], {k: v['gbps'] for k, v in c['other_configs'].items()}, c['single_launch'], c['final_gather'], d['cpu_baseline']['matches_gpu'], c['parity']['all_match'], c['parity']['mismatching_paths'], c['parity']['seconds'])"

@@ -64,10 +64,32 @@ static int check_table(const std::vector<uint32_t>& t, const std::vector<uint32_
     return 0;
 }
 
+// thirds table: each CU gets exactly one 4-chunk workgroup (and 7 of 3 chunks) under both dealing orders of
+// an XCD's 256 workgroups to its 32 CUs: round robin (CU n % 32) and 8 at a time (CU n / 8)
+static int check_thirds_per_cu(const std::vector<uint32_t>& t)
+{
+    const int nwg = (int)t.size() - 1;
+    for (int order = 0; order < 2; order++) {
+        std::vector<int> four(nwg / 8), total(nwg / 8);  // per (XCD, CU)
+        for (int g = 0; g < nwg; g++) {
+            const int x = g % 8, n = g / 8, cu = order == 0 ? n % 32 : n / 8;
+            total[x * 32 + cu]++;
+            if (t[g + 1] - t[g] == 4) four[x * 32 + cu]++;
+        }
+        for (int c = 0; c < nwg / 8; c++)
+            if (four[c] != 1 || total[c] != 8) {
+                printf("FAIL thirds: CU %d gets %d 4-chunk workgroups of %d (dealing order %d)\n", c, four[c], total[c], order);
+                return 1;
+            }
+    }
+    return 0;
+}
+
 int main()
 {
     int bad = 0;
     const int nsimd = 1024;  // 256 CUs
+    bad |= check_thirds_per_cu(seg_table(nsimd, true));
     for (int thirds = 0; thirds < 2; thirds++) {
         const std::vector<uint32_t> t = seg_table(nsimd, thirds == 1);
         if (t.empty() || t.back() != (uint32_t)kChunks) { printf("FAIL table %d\n", thirds); return 1; }
