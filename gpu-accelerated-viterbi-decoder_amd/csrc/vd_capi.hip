@@ -185,7 +185,7 @@ struct vd_decoder {
     size_t cap2_in = 0, cap2_out = 0;
     hipStream_t s_in = nullptr, s_out = nullptr;
     DeviceState* ds = nullptr;  // the device's board / segment tables (looked up once, vd_create)
-    int split = 1;              // segment launches: 0 none (VD_NO_SPLIT=1), 1 pieces, 2 thirds (VD_SPLIT=...)
+    int split = 1;              // segment launches: 0 none (VD_NO_SPLIT=1), 1 pieces, 2 thirds, 3 sevenths (VD_SPLIT=...)
     uint32_t* check = nullptr;  // LDS guard violation counter (vd_set_guard_check), null = off
 };
 
@@ -224,7 +224,7 @@ struct DeviceState {
     uint32_t* board = nullptr;
     int nsimd = 0;
     uint32_t* stats = nullptr;
-    SegTable pieces, thirds;
+    SegTable pieces, thirds, sevenths;
 };
 static DeviceState* device_state(int device)
 {
@@ -241,10 +241,10 @@ static DeviceState* device_state(int device)
         bool ok = hipMalloc(&x->board, vd::kFairBoardWords * 4) == hipSuccess &&
                   hipMemset(x->board, 0xFF, vd::kFairBoardWords * 4) == hipSuccess &&
                   hipMalloc(&x->stats, 4) == hipSuccess && hipMemset(x->stats, 0, 4) == hipSuccess;
-        for (int th = 0; th < 2 && ok; th++) {
-            const std::vector<uint32_t> t = vd::seg_table(x->nsimd, th == 1);
+        for (int th = 0; th < 3 && ok; th++) {
+            const std::vector<uint32_t> t = vd::seg_table(x->nsimd, th);
             if (t.empty()) continue;
-            SegTable& T = th ? x->thirds : x->pieces;
+            SegTable& T = th == vd::kSegSevenths ? x->sevenths : th == vd::kSegThirds ? x->thirds : x->pieces;
             ok = hipMalloc(&T.d, t.size() * 4) == hipSuccess &&
                  hipMemcpy(T.d, t.data(), t.size() * 4, hipMemcpyHostToDevice) == hipSuccess;
             T.nwg = (unsigned)(t.size() - 1);
@@ -263,7 +263,7 @@ static unsigned plan_split(vd::Geom& g, int options, const DeviceState* x, int m
     const uint64_t words32 = out_of(options) != 0 ? g.packNum / 2 : g.packNum;  // O_B16: 16-bit words
     if (mode == 0 || g.nchunks != (uint32_t)vd::kChunks || words32 / g.nchunks < (uint64_t)vd::kSplitMinWords)
         return tg_grid(g);
-    const SegTable& T = mode == 2 && x->thirds.d ? x->thirds : x->pieces;
+    const SegTable& T = mode == 2 && x->thirds.d ? x->thirds : mode == 3 && x->sevenths.d ? x->sevenths : x->pieces;
     if (!T.d) return tg_grid(g);
     g.seg = T.d;
     g.stats = x->stats;
@@ -352,7 +352,7 @@ int vd_create(int options, size_t preallocInputNum, int device, vd_decoder** out
     }
     const char* nosplit = std::getenv("VD_NO_SPLIT");
     const char* smode = std::getenv("VD_SPLIT");
-    d->split = nosplit && nosplit[0] == '1' ? 0 : smode && !strcmp(smode, "thirds") ? 2 : 1;
+    d->split = nosplit && nosplit[0] == '1' ? 0 : smode && !strcmp(smode, "thirds") ? 2 : smode && !strcmp(smode, "sevenths") ? 3 : 1;
     const char* chk = std::getenv("VD_CHECK");
     if (chk && chk[0] == '1') {
         int rc = vd_set_guard_check(d, 1);

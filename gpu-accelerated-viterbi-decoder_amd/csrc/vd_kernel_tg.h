@@ -46,6 +46,9 @@ constexpr int kAblNoTraceback = 1, kAblNoTabReads = 2, kAblNoReadout = 4, kAblNo
               kAblClock = 32, kAblNoFair = 256, kAblNoTabWrites = 512;
 // layout variant (tools A/B; an exact twin of the product)
 constexpr int kAblPostExchange = 8192;  // LDS-exchange stages exchange V and subtract after (round 2)
+// exchange variants (exact twins): the xor-32 / xor-16 stage by a VALU lane swap (v_permlane32_swap /
+// v_permlane16_swap) instead of the LDS crossbar: more VALU issue, no LDS round trip in the chain
+constexpr int kAblX32Perm = 16384, kAblX16Perm = 32768;
 constexpr int kAblAcsOnly = kAblNoTraceback | kAblNoTabReads | kAblNoReadout | kAblNoTabBuild | kAblNoLoads;
 
 template <int CH>
@@ -220,6 +223,36 @@ __device__ __forceinline__ void tg_stage_lds_sg(float& V, float m, float vp, flo
     float t1, t2;
     asm("v_fma_f32 %1, %3, %5, %0\n\tv_fma_f32 %2, -%3, %5, %4\n\tv_max_f32 %0, %1, %2"
         : "+{v60}"(V), "=&v"(t1), "=&v"(t2) : "v"(m), "v"(vp), "v"(sg));
+}
+
+// The xor-32 / xor-16 stage by a VALU lane swap.  v_permlane32_swap t, u exchanges lanes 32..63 of t with
+// lanes 0..31 of u (v_permlane16_swap: the odd rows of t with the even rows of u).  With the sign s = +1 in
+// the lower member of every exchange pair (lane bit 5 / 4 clear) and -1 in the upper one, t = V + s m and
+// u = V - s m become (own V + m, partner V - m) in every lane after the swap: V' = max(t, u).  The partners
+// share label and tag (every stage but M_B32's phase 0, below).
+template <bool X32>
+__device__ __forceinline__ void tg_stage_perm(float& V, float m, float s)
+{
+    float t, u;
+    if constexpr (X32)
+        asm("v_fma_f32 %1, %3, %4, %0\n\tv_fma_f32 %2, -%3, %4, %0\n\ts_nop 1\n\tv_permlane32_swap_b32 %1, %2\n\t"
+            "v_max_f32 %0, %1, %2"
+            : "+{v60}"(V), "=&v"(t), "=&v"(u) : "v"(s), "v"(m));
+    else
+        asm("v_fma_f32 %1, %3, %4, %0\n\tv_fma_f32 %2, -%3, %4, %0\n\ts_nop 1\n\tv_permlane16_swap_b32 %1, %2\n\t"
+            "v_max_f32 %0, %1, %2"
+            : "+{v60}"(V), "=&v"(t), "=&v"(u) : "v"(s), "v"(m));
+}
+// M_B32 phase 0 (S32) by the lane swap: swapped copies of V put the lower member's metric x in the first
+// and the upper member's y in the second register of every lane; both halves then take max(x + m, y - m)
+// (the lower half's own entry m is E[L]; the upper half's is E[3 - L] and its roles are reversed, see
+// tg_stage_lds_sg)
+__device__ __forceinline__ void tg_stage_perm_sg(float& V, float m)
+{
+    float y, t, u;
+    asm("v_mov_b32 %1, %0\n\ts_nop 1\n\tv_permlane32_swap_b32 %0, %1\n\tv_add_f32 %2, %0, %4\n\t"
+        "v_sub_f32 %3, %1, %4\n\tv_max_f32 %0, %2, %3"
+        : "+{v60}"(V), "=&v"(y), "=&v"(t), "=&v"(u) : "v"(m));
 }
 
 // int32 stages (TgFmt::INT): the same forms on integer patterns
@@ -415,8 +448,10 @@ struct TgIn<SOFT8> {  // 2 stages per word; the 16-bit half g^1 holds s0 (high b
     static constexpr bool S01 = true;
     static __device__ __forceinline__ void s01(raw_t w, float& s0, float& s1)
     {
-        s0 = (float)(int)(int8_t)(uint8_t)(w >> 8);  // v_lshlrev + v_cvt_f32_i32_sdwa sext BYTE_3
-        s1 = (float)(int)(int8_t)(uint8_t)w;         // v_cvt_f32_i32_sdwa sext BYTE_0
+        // one sign-extending byte convert each (left to itself the compiler shifted byte 1 up to byte 3
+        // first: one VALU op more per table row)
+        asm("v_cvt_f32_i32_sdwa %0, sext(%1) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_1" : "=v"(s0) : "v"(w));
+        asm("v_cvt_f32_i32_sdwa %0, sext(%1) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_0" : "=v"(s1) : "v"(w));
     }
 };
 template <>
@@ -699,6 +734,7 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(8))
     // INT, label regions: the upper half's phase-0 entries come from the +tag area
     if constexpr (INT) aK[0] = upper5 ? TgTabLT<true>::ALT_OFF + 8 * own_label(pos, 0) : aK[0];
     const float sg0 = upper5 ? -1.0f : 1.0f;                  // S32: sign of the phase-0 entry
+    const float sg4 = (pos >> 4) & 1 ? -1.0f : 1.0f;          // kAblX16Perm: upper member of an xor-16 pair
     const int pa5 = 4 * (lane ^ 32);           // ds_bpermute address of the xor-32 partner
     const uint32_t tbk = tb_pack<J, CORE == B32>(lane);  // traceback constants of word kb + lane (kb % 3 == 0)
     // table-build roles: lane l builds the entries at table index l (stage sA) and, lanes 0..31, index
@@ -804,6 +840,9 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(8))
                 else tg_stage_lds_i(V, m, tg_partner(V, pa5));
             } else {
                 if constexpr (Q <= 3) tg_stage_dpp2<Q>(V, m);
+                else if constexpr (Q == 4 && (ABL & kAblX16Perm)) tg_stage_perm<false>(V, m, sg4);
+                else if constexpr (Q == 5 && (ABL & kAblX32Perm) && S32) tg_stage_perm_sg(V, m);
+                else if constexpr (Q == 5 && (ABL & kAblX32Perm)) tg_stage_perm<true>(V, m, sg0);
                 else if constexpr (Q == 4 && PRE) tg_stage_lds_pre<false, false>(V, m, pa5);
                 else if constexpr (Q == 4) tg_stage_lds(V, m, tg_swz16(V));
                 else if constexpr (S32) tg_stage_lds_sg(V, m, tg_partner(V, pa5), sg0);

@@ -69,37 +69,37 @@ def lib():
         if stale:
             raise VitdecError(f"{LIB_PATH} is stale ({stale}): rebuild it with `make -C {_HERE}`")
     sz, vp, i, f = ctypes.c_size_t, ctypes.c_void_p, ctypes.c_int, ctypes.c_float
-    L.vd_options_valid.argtypes = [i]
-    for n in ("vd_input_size", "vd_message_len", "vd_output_size"):
-        getattr(L, n).argtypes = [i, sz]
-        getattr(L, n).restype = sz
-    L.vd_create.argtypes = [i, sz, i, ctypes.POINTER(vp)]
-    L.vd_destroy.argtypes = [vp]
-    L.vd_run.argtypes = [vp, vp, vp, sz, ctypes.POINTER(f)]
-    L.vd_run_device.argtypes = [vp, vp, vp, sz, vp]
-    L.vd_run_device_batch.argtypes = [vp, vp, sz, vp, sz, sz, ctypes.c_int, vp]
-    L.vd_run_batches.argtypes = [i, ctypes.POINTER(vp), ctypes.POINTER(vp), sz, i, ctypes.POINTER(i), i,
-                                 ctypes.POINTER(f)]
-    L.vd_simulate_host.argtypes = [i, sz, f, ctypes.c_uint32, ctypes.c_uint32, vp, vp]
-    L.vd_channel_device.argtypes = [sz, f, ctypes.c_uint32, ctypes.c_uint32, vp, vp, vp]
-    L.vd_simulate_device.argtypes = [i, sz, f, ctypes.c_uint32, ctypes.c_uint32, vp, vp, vp]
-    L.vd_mt_state_after.argtypes = [ctypes.c_uint32, ctypes.c_uint64, vp]
-    L.vd_split_redecodes.argtypes = [i, ctypes.POINTER(ctypes.c_uint64)]
-    L.vd_set_guard_check.argtypes = [vp, i]
-    L.vd_guard_violations.argtypes = [vp, ctypes.POINTER(ctypes.c_uint64)]
-    L.vd_count_errors.argtypes = [i, vp, sz, vp, sz]
-    L.vd_count_errors.restype = ctypes.c_longlong
-    L.vd_last_error.restype = ctypes.c_char_p
-    L.vd_pack_device.argtypes = [i, vp, sz, f, vp, vp]
-    L.vd_host_alloc.argtypes = [sz]
-    L.vd_host_alloc.restype = vp
-    L.vd_host_free.argtypes = [vp]
-    L.vd_run_stream.argtypes = [vp, ctypes.POINTER(vp), ctypes.POINTER(vp), i, sz, ctypes.POINTER(f)]
-    L.vd_run_device_llr.argtypes = [vp, vp, vp, sz, f, vp]
-    L.vd_run_llr.argtypes = [vp, vp, vp, sz, f, ctypes.POINTER(f)]
-    L.vd_run_device_llr_batch.argtypes = [vp, vp, sz, vp, sz, sz, f, ctypes.c_int, vp]
-    L.vd_kernel_name.argtypes = [i]
-    L.vd_kernel_name.restype = ctypes.c_char_p
+    # name: (argtypes, restype or None)
+    sig = {"vd_options_valid": ([i], None),
+           "vd_input_size": ([i, sz], sz), "vd_message_len": ([i, sz], sz), "vd_output_size": ([i, sz], sz),
+           "vd_create": ([i, sz, i, ctypes.POINTER(vp)], None), "vd_destroy": ([vp], None),
+           "vd_run": ([vp, vp, vp, sz, ctypes.POINTER(f)], None), "vd_run_device": ([vp, vp, vp, sz, vp], None),
+           "vd_run_device_batch": ([vp, vp, sz, vp, sz, sz, ctypes.c_int, vp], None),
+           "vd_run_batches": ([i, ctypes.POINTER(vp), ctypes.POINTER(vp), sz, i, ctypes.POINTER(i), i,
+                               ctypes.POINTER(f)], None),
+           "vd_simulate_host": ([i, sz, f, ctypes.c_uint32, ctypes.c_uint32, vp, vp], None),
+           "vd_channel_device": ([sz, f, ctypes.c_uint32, ctypes.c_uint32, vp, vp, vp], None),
+           "vd_simulate_device": ([i, sz, f, ctypes.c_uint32, ctypes.c_uint32, vp, vp, vp], None),
+           "vd_mt_state_after": ([ctypes.c_uint32, ctypes.c_uint64, vp], None),
+           "vd_split_redecodes": ([i, ctypes.POINTER(ctypes.c_uint64)], None),
+           "vd_set_guard_check": ([vp, i], None), "vd_guard_violations": ([vp, ctypes.POINTER(ctypes.c_uint64)], None),
+           "vd_count_errors": ([i, vp, sz, vp, sz], ctypes.c_longlong), "vd_last_error": (None, ctypes.c_char_p),
+           "vd_pack_device": ([i, vp, sz, f, vp, vp], None), "vd_host_alloc": ([sz], vp), "vd_host_free": ([vp], None),
+           "vd_run_stream": ([vp, ctypes.POINTER(vp), ctypes.POINTER(vp), i, sz, ctypes.POINTER(f)], None),
+           "vd_run_device_llr": ([vp, vp, vp, sz, f, vp], None),
+           "vd_run_llr": ([vp, vp, vp, sz, f, ctypes.POINTER(f)], None),
+           "vd_run_device_llr_batch": ([vp, vp, sz, vp, sz, sz, f, ctypes.c_int, vp], None),
+           "vd_kernel_name": ([i], ctypes.c_char_p)}
+    for name, (args, res) in sig.items():
+        if not hasattr(L, name):
+            if os.environ.get("VITDEC_LIB"):  # an earlier round's build in a same-box A/B: fewer entry points
+                continue
+            raise VitdecError(f"{LIB_PATH} does not export {name}")
+        fn = getattr(L, name)
+        if args is not None:
+            fn.argtypes = args
+        if res is not None:
+            fn.restype = res
     _lib = L
     return L
 

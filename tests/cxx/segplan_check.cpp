@@ -64,21 +64,22 @@ static int check_table(const std::vector<uint32_t>& t, const std::vector<uint32_
     return 0;
 }
 
-// thirds table: each CU gets exactly one 4-chunk workgroup (and 7 of 3 chunks) under both dealing orders of
-// an XCD's 256 workgroups to its 32 CUs: round robin (CU n % 32) and 8 at a time (CU n / 8)
-static int check_thirds_per_cu(const std::vector<uint32_t>& t)
+// thirds / sevenths tables: each CU gets the intended mix of 4-chunk workgroups -- thirds: 1 of 8 (7 of 3
+// chunks), sevenths: 4 of 7 (3 of 3 chunks) -- under both dealing orders of an XCD's workgroups to its 32
+// CUs: round robin (CU n % 32) and per CU a run of consecutive n (CU n / per-CU count)
+static int check_mix_per_cu(const std::vector<uint32_t>& t, int perCu, int wantFour, const char* name)
 {
-    const int nwg = (int)t.size() - 1;
+    const int nwg = (int)t.size() - 1, ncu = nwg / perCu;  // CUs of the chip (8 XCDs x 32)
     for (int order = 0; order < 2; order++) {
-        std::vector<int> four(nwg / 8), total(nwg / 8);  // per (XCD, CU)
+        std::vector<int> four(ncu), total(ncu);  // per (XCD, CU)
         for (int g = 0; g < nwg; g++) {
-            const int x = g % 8, n = g / 8, cu = order == 0 ? n % 32 : n / 8;
+            const int x = g % 8, n = g / 8, cu = order == 0 ? n % 32 : n / perCu;
             total[x * 32 + cu]++;
             if (t[g + 1] - t[g] == 4) four[x * 32 + cu]++;
         }
-        for (int c = 0; c < nwg / 8; c++)
-            if (four[c] != 1 || total[c] != 8) {
-                printf("FAIL thirds: CU %d gets %d 4-chunk workgroups of %d (dealing order %d)\n", c, four[c], total[c], order);
+        for (int c = 0; c < ncu; c++)
+            if (four[c] != wantFour || total[c] != perCu) {
+                printf("FAIL %s: CU %d gets %d 4-chunk workgroups of %d (dealing order %d)\n", name, c, four[c], total[c], order);
                 return 1;
             }
     }
@@ -89,10 +90,11 @@ int main()
 {
     int bad = 0;
     const int nsimd = 1024;  // 256 CUs
-    bad |= check_thirds_per_cu(seg_table(nsimd, true));
-    for (int thirds = 0; thirds < 2; thirds++) {
-        const std::vector<uint32_t> t = seg_table(nsimd, thirds == 1);
-        if (t.empty() || t.back() != (uint32_t)kChunks) { printf("FAIL table %d\n", thirds); return 1; }
+    bad |= check_mix_per_cu(seg_table(nsimd, kSegThirds), 8, 1, "thirds");
+    bad |= check_mix_per_cu(seg_table(nsimd, kSegSevenths), 7, 4, "sevenths");
+    for (int mode = 0; mode < 3; mode++) {
+        const std::vector<uint32_t> t = seg_table(nsimd, mode);
+        if (t.empty() || t.back() != (uint32_t)kChunks) { printf("FAIL table %d\n", mode); return 1; }
         // the bench sizes (32M and 16M bits, O_B32 and O_B16) and random word counts >= kSplitMinWords
         std::vector<uint32_t> packs = {999998, 499998, 1999996 / 2, 7999996 / 2};
         srand(7);

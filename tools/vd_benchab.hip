@@ -72,7 +72,7 @@ int main(int argc, char** argv)
     {   // single launches: the product's segment table (round 2's pieces)
         int cus = 0;
         CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
-        const std::vector<uint32_t> t = vd::seg_table(4 * cus, false);
+        const std::vector<uint32_t> t = vd::seg_table(4 * cus, vd::kSegPieces);
         uint32_t* tb; CK(hipMalloc(&tb, t.size() * 4));
         CK(hipMemcpy(tb, t.data(), t.size() * 4, hipMemcpyHostToDevice));
         g.seg = tb;

@@ -53,7 +53,7 @@ int main(int argc, char** argv)
     uint32_t* tab[NM] = {nullptr};
     unsigned grid[NM] = {1600, 0, 0, 0, 0};
     for (int m = 1; m < NM; m++) {
-        std::vector<uint32_t> t = vd::seg_table(4 * cus, thirdsOf[m]);
+        std::vector<uint32_t> t = vd::seg_table(4 * cus, thirdsOf[m] ? vd::kSegThirds : vd::kSegPieces);
         if (t.empty()) { printf("no %s table for %d CUs\n", names[m], cus); return 1; }
         CK(hipMalloc(&tab[m], t.size() * 4));
         CK(hipMemcpy(tab[m], t.data(), t.size() * 4, hipMemcpyHostToDevice));
