@@ -49,6 +49,9 @@ constexpr int kAblPostExchange = 8192;  // LDS-exchange stages exchange V and su
 // exchange variants (exact twins): the xor-32 / xor-16 stage by a VALU lane swap (v_permlane32_swap /
 // v_permlane16_swap) instead of the LDS crossbar: more VALU issue, no LDS round trip in the chain
 constexpr int kAblX32Perm = 16384, kAblX16Perm = 32768;
+// max on the integer patterns (v_max_u32: the metrics are positive normal floats of one binade, so the
+// integer order is the float order): an exact twin
+constexpr int kAblIntMax = 65536;
 constexpr int kAblAcsOnly = kAblNoTraceback | kAblNoTabReads | kAblNoReadout | kAblNoTabBuild | kAblNoLoads;
 
 template <int CH>
@@ -167,18 +170,22 @@ typedef float f2v __attribute__((ext_vector_type(2)));
 // b = V - m, and the max takes b from the partner through the DPP operand, V' = max(a, dpp(b)).  b is
 // read by DPP 2 slots after its write.  (The three-op form v_add, v_sub_f32_dpp, v_max decides the same;
 // this one is 0.5-1 % faster, profiles/r02/benchab_dpp_forms_8w.log.)
-template <int Q>
+template <int Q, bool IM = false>
 __device__ __forceinline__ void tg_stage_dpp2(float& V, float m)
 {
     float a, b;
-#define VD_TG_DPP2(CTRL)                                                                                     \
+#define VD_TG_DPP2(MAX, CTRL)                                                                                \
     asm("v_sub_f32 %2, %0, %3\n\tv_add_f32 %1, %0, %3\n\ts_nop 0\n\t"                                      \
-        "v_max_f32_dpp %0, %2, %1 " CTRL " row_mask:0xf bank_mask:0xf"                                         \
+        MAX " %0, %2, %1 " CTRL " row_mask:0xf bank_mask:0xf"                                                  \
         : "+{v60}"(V), "=&v"(a), "=&v"(b) : "v"(m))
-    if constexpr (Q == 0) VD_TG_DPP2("quad_perm:[1,0,3,2]");
-    else if constexpr (Q == 1) VD_TG_DPP2("quad_perm:[2,3,0,1]");
-    else if constexpr (Q == 2) VD_TG_DPP2("row_half_mirror");
-    else VD_TG_DPP2("row_ror:8");
+#define VD_TG_DPP2Q(MAX)                                                                                     \
+    if constexpr (Q == 0) VD_TG_DPP2(MAX, "quad_perm:[1,0,3,2]");                                            \
+    else if constexpr (Q == 1) VD_TG_DPP2(MAX, "quad_perm:[2,3,0,1]");                                       \
+    else if constexpr (Q == 2) VD_TG_DPP2(MAX, "row_half_mirror");                                           \
+    else VD_TG_DPP2(MAX, "row_ror:8");
+    if constexpr (IM) { VD_TG_DPP2Q("v_max_u32_dpp") }
+    else { VD_TG_DPP2Q("v_max_f32_dpp") }
+#undef VD_TG_DPP2Q
 #undef VD_TG_DPP2
 }
 
@@ -204,7 +211,7 @@ __device__ __forceinline__ void tg_stage_lds(float& V, float m, float vp)
 // with its per-half tag sign), the received value is V_partner - m.  After the exchange returns only the
 // max is left, so the round trip's dependent chain is one op shorter; a = V + m issues while it is in
 // flight.
-template <bool X32, bool INT>
+template <bool X32, bool INT, bool IM = false>
 __device__ __forceinline__ void tg_stage_lds_pre(float& V, float m, int paddr)
 {
     float a, b;
@@ -214,15 +221,21 @@ __device__ __forceinline__ void tg_stage_lds_pre(float& V, float m, int paddr)
     if constexpr (INT) asm("v_add_u32 %0, %1, %2" : "=v"(a) : "v"(V), "v"(m));
     else asm("v_add_f32 %0, %1, %2" : "=v"(a) : "v"(V), "v"(m));
     if constexpr (INT) asm("v_max_i32 %0, %1, %2" : "={v60}"(V) : "v"(a), "v"(bp));
+    else if constexpr (IM) asm("v_max_u32 %0, %1, %2" : "={v60}"(V) : "v"(a), "v"(bp));
     else asm("v_max_f32 %0, %1, %2" : "={v60}"(V) : "v"(a), "v"(bp));
 }
 // M_B32 phase-0 stage (S32): V' = max(V + s*m, vp - s*m), s = -1 in the upper position half, where m is
 // the entry of the complementary label (see the kernel)
+template <bool IM = false>
 __device__ __forceinline__ void tg_stage_lds_sg(float& V, float m, float vp, float sg)
 {
     float t1, t2;
-    asm("v_fma_f32 %1, %3, %5, %0\n\tv_fma_f32 %2, -%3, %5, %4\n\tv_max_f32 %0, %1, %2"
-        : "+{v60}"(V), "=&v"(t1), "=&v"(t2) : "v"(m), "v"(vp), "v"(sg));
+    if constexpr (IM)
+        asm("v_fma_f32 %1, %3, %5, %0\n\tv_fma_f32 %2, -%3, %5, %4\n\tv_max_u32 %0, %1, %2"
+            : "+{v60}"(V), "=&v"(t1), "=&v"(t2) : "v"(m), "v"(vp), "v"(sg));
+    else
+        asm("v_fma_f32 %1, %3, %5, %0\n\tv_fma_f32 %2, -%3, %5, %4\n\tv_max_f32 %0, %1, %2"
+            : "+{v60}"(V), "=&v"(t1), "=&v"(t2) : "v"(m), "v"(vp), "v"(sg));
 }
 
 // The xor-32 / xor-16 stage by a VALU lane swap.  v_permlane32_swap t, u exchanges lanes 32..63 of t with
@@ -839,14 +852,15 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(8))
                 else if constexpr (Q == 4) tg_stage_lds_i(V, m, tg_swz16(V));
                 else tg_stage_lds_i(V, m, tg_partner(V, pa5));
             } else {
-                if constexpr (Q <= 3) tg_stage_dpp2<Q>(V, m);
+                constexpr bool IM = (ABL & kAblIntMax) != 0;
+                if constexpr (Q <= 3) tg_stage_dpp2<Q, IM>(V, m);
                 else if constexpr (Q == 4 && (ABL & kAblX16Perm)) tg_stage_perm<false>(V, m, sg4);
                 else if constexpr (Q == 5 && (ABL & kAblX32Perm) && S32) tg_stage_perm_sg(V, m);
                 else if constexpr (Q == 5 && (ABL & kAblX32Perm)) tg_stage_perm<true>(V, m, sg0);
-                else if constexpr (Q == 4 && PRE) tg_stage_lds_pre<false, false>(V, m, pa5);
+                else if constexpr (Q == 4 && PRE) tg_stage_lds_pre<false, false, IM>(V, m, pa5);
                 else if constexpr (Q == 4) tg_stage_lds(V, m, tg_swz16(V));
-                else if constexpr (S32) tg_stage_lds_sg(V, m, tg_partner(V, pa5), sg0);
-                else if constexpr (PRE) tg_stage_lds_pre<true, false>(V, m, pa5);
+                else if constexpr (S32) tg_stage_lds_sg<IM>(V, m, tg_partner(V, pa5), sg0);
+                else if constexpr (PRE) tg_stage_lds_pre<true, false, IM>(V, m, pa5);
                 else tg_stage_lds(V, m, tg_partner(V, pa5));
             }
             if constexpr (r + TGD < 96) issue(std::integral_constant<int, r + TGD>{});

@@ -27,10 +27,8 @@ struct V {
 struct Variant { const char* name; KFn hard, soft8; int seg = vd::kSegPieces; uint32_t warm = vd::kSplitWarm; };
 #ifndef VD_ABX_VARIANTS
 #define VD_ABX_VARIANTS                                                                                      \
-    {"product (pieces, 6 warm-up blocks)", V<0>::hard, V<0>::soft8},                                         \
-    {"sevenths, 6 warm-up blocks", V<0>::hard, V<0>::soft8, vd::kSegSevenths, 6},                            \
-    {"sevenths, 3 warm-up blocks", V<0>::hard, V<0>::soft8, vd::kSegSevenths, 3},                            \
-    {"thirds, 6 warm-up blocks", V<0>::hard, V<0>::soft8, vd::kSegThirds, 6},
+    {"product", V<0>::hard, V<0>::soft8},                                                                    \
+    {"max on integer patterns (v_max_u32)", V<vd::kAblIntMax>::hard, V<vd::kAblIntMax>::soft8},
 #endif
 
 static double median(std::vector<float> v)
