@@ -52,6 +52,8 @@ constexpr int kAblX32Perm = 16384, kAblX16Perm = 32768;
 // max on the integer patterns (v_max_u32: the metrics are positive normal floats of one binade, so the
 // integer order is the float order): an exact twin
 constexpr int kAblIntMax = 65536;
+// latency studies (tools): table reads 8 stages ahead instead of 4; fairness controller every 4th group head
+constexpr int kAblTgd8 = 131072, kAblFair4 = 262144;
 constexpr int kAblAcsOnly = kAblNoTraceback | kAblNoTabReads | kAblNoReadout | kAblNoTabBuild | kAblNoLoads;
 
 template <int CH>
@@ -818,7 +820,7 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(8))
     // ahead; one ds_read_b64 at an even period also carries the entry of the stage 6 later.  The
     // loads are volatile LDS-address-space loads so they stay single ds_read_b64s (2 LDS cycles) in
     // program order -- left alone the compiler merges neighbours into ds_read2_b64 (8 cycles).
-    constexpr int TGD = 4;  // 6 or 8 measured the same (profiles/r02/ablate_prefetch.log)
+    constexpr int TGD = (ABL & kAblTgd8) ? 8 : 4;  // 6 or 8 measured the same (profiles/r02/ablate_prefetch.log)
     typedef __attribute__((address_space(3))) const volatile f2v* lptr;
     const __attribute__((address_space(3))) char* tl = (const __attribute__((address_space(3))) char*)tabb;
     f2v vp[96];  // entry pair read for stage r (the even period of a period pair)
@@ -1000,7 +1002,7 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(8))
         // every other group head (6 blocks): 0.7 % faster than every head, every third is 1 % slower
         // (profiles/r02/benchab_fair.log)
         if constexpr (!(ABL & kAblNoFair))
-            if ((j / 3) % 2 == 0) fair.group((fdone + j) * fscale, 3u * fscale, lane);
+            if ((j / 3) % ((ABL & kAblFair4) ? 4 : 2) == 0) fair.group((fdone + j) * fscale, 3u * fscale, lane);
         if (split && pass == 0 && (int)j == Xspec) vS = V;
         if (split && (int)j == Xcmp) vE = V;
         wave_sync();

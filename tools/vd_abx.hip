@@ -28,7 +28,9 @@ struct Variant { const char* name; KFn hard, soft8; int seg = vd::kSegPieces; ui
 #ifndef VD_ABX_VARIANTS
 #define VD_ABX_VARIANTS                                                                                      \
     {"product", V<0>::hard, V<0>::soft8},                                                                    \
-    {"max on integer patterns (v_max_u32)", V<vd::kAblIntMax>::hard, V<vd::kAblIntMax>::soft8},
+    {"table reads 8 stages ahead", V<vd::kAblTgd8>::hard, V<vd::kAblTgd8>::soft8},                           \
+    {"fairness every 4th group head", V<vd::kAblFair4>::hard, V<vd::kAblFair4>::soft8},                      \
+    {"no fairness controller", V<vd::kAblNoFair>::hard, V<vd::kAblNoFair>::soft8},
 #endif
 
 static double median(std::vector<float> v)
