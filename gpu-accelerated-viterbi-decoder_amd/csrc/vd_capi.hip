@@ -21,6 +21,7 @@
 #include "../../include/vd_capi.h"
 #include "vd_kernels.h"
 #include "vd_kernel_tg.h"
+#include "vd_kernel_pk.h"
 #include "vd_pack.h"
 #include "vd_mt.h"
 #include "vd_mtjump.h"
@@ -118,6 +119,19 @@ launch_fn pick_ob(int ob)
     return ob == 1 ? &launch_t<CH, CORE, 16> : &launch_t<CH, CORE, 32>;
 }
 
+// batched HARD / 32-bit-output launches: two chunks per wave in int16 halves (vd_kernel_pk.h)
+template <int CORE>
+void launch_pk(const void* in, void* out, vd::Geom g, unsigned grid, hipStream_t s)
+{
+    hipLaunchKernelGGL((vd::vd_decode_pk<CORE>), dim3(grid), dim3(64 * vd::kWaves), 0, s, in, out, g);
+}
+launch_fn pick_pk(int o)
+{
+    if (ch_of(o) != 0 || out_of(o) != 0) return nullptr;
+    const int me = met_of(o);
+    return me == 0 ? &launch_pk<0> : me == 1 ? &launch_pk<1> : &launch_pk<2>;
+}
+
 template <int L>
 launch_fn pick_ch(int o)
 {
@@ -141,8 +155,12 @@ launch_fn pick(int o, bool llr)
 const char* kname(int o)
 {
     static const char* names[5][3] = {
-        {"vd_decode_tg<HARD,B32> (fp32 tagged core, M_B32 tie rule)", "vd_decode_tg<HARD,B16> (fp32 tagged core, M_B16 tie rule)",
-         "vd_decode_tg<HARD,F16> (fp32 tagged core, M_FP16 tie rule)"},
+        {"vd_decode_pk<B32> (batched: two chunks per lane in int16 halves) / vd_decode_tg<HARD,B32> (single batch: "
+         "fp32 tagged core); M_B32 tie rule",
+         "vd_decode_pk<B16> (batched: two chunks per lane in int16 halves) / vd_decode_tg<HARD,B16> (single batch: "
+         "fp32 tagged core); M_B16 tie rule",
+         "vd_decode_pk<F16> (batched: two chunks per lane in int16 halves) / vd_decode_tg<HARD,F16> (single batch: "
+         "fp32 tagged core); M_FP16 tie rule"},
         {"vd_decode_tg<SOFT4,B32> (fp32 tagged core, M_B32 tie rule)", "vd_decode_tg<SOFT4,B16> (fp32 tagged core, M_B16 tie rule)",
          "vd_decode_tg<SOFT4,F16> (fp32 tagged core, M_FP16 tie rule)"},
         {"vd_decode_tg<SOFT8,B32> (fp32 tagged core, M_B32 tie rule)", "vd_decode_tg<SOFT8,B16> (fp32 tagged core, M_B16 tie rule)", "-"},
@@ -186,6 +204,7 @@ struct vd_decoder {
     hipStream_t s_in = nullptr, s_out = nullptr;
     DeviceState* ds = nullptr;  // the device's board / segment tables (looked up once, vd_create)
     int split = 1;              // segment launches: 0 none (VD_NO_SPLIT=1), 1 pieces, 2 thirds, 3 sevenths (VD_SPLIT=...)
+    int pk = 1;                 // batched HARD launches on vd_decode_pk (VD_NO_PK=1: on vd_decode_tg)
     uint32_t* check = nullptr;  // LDS guard violation counter (vd_set_guard_check), null = off
 };
 
@@ -299,6 +318,12 @@ static int launch_decode(const vd_decoder* d, const void* in_d, void* out_d, siz
     g.nbatch = nbatch;
     g.inStride = inStride;
     g.outStride = outStride;
+    launch_fn fp = nbatch > 1 && !llr && d->pk && g.nchunks % (2 * vd::kWaves) == 0 ? pick_pk(options) : nullptr;
+    if (fp) {  // two chunks per wave: nchunks * nbatch / 8 workgroups
+        fp(in_d, out_d, g, (unsigned)((uint64_t)g.nchunks * nbatch / (2 * vd::kWaves)), s);
+        VD_HIP(hipGetLastError());
+        return VD_OK;
+    }
     const unsigned grid = nbatch == 1 ? plan_split(g, options, d->ds, d->split) : tg_grid(g);
     f(in_d, out_d, g, grid, s);
     VD_HIP(hipGetLastError());
@@ -353,6 +378,8 @@ int vd_create(int options, size_t preallocInputNum, int device, vd_decoder** out
     const char* nosplit = std::getenv("VD_NO_SPLIT");
     const char* smode = std::getenv("VD_SPLIT");
     d->split = nosplit && nosplit[0] == '1' ? 0 : smode && !strcmp(smode, "thirds") ? 2 : smode && !strcmp(smode, "sevenths") ? 3 : 1;
+    const char* nopk = std::getenv("VD_NO_PK");
+    d->pk = nopk && nopk[0] == '1' ? 0 : 1;
     const char* chk = std::getenv("VD_CHECK");
     if (chk && chk[0] == '1') {
         int rc = vd_set_guard_check(d, 1);

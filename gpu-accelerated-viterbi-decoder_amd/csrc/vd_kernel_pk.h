@@ -1,0 +1,267 @@
+// vd_kernel_pk.h -- vd_decode_pk<CORE>: HARD input, TWO chunks per wave, one in each 16-bit half of the
+// lane's metric word (batched launches).  Same decode as vd_decode_tg<HARD, CORE, 32> word for word
+// (reference viterbi_core, src/viterbi/viterbi.cu:144-207; tie rules viterbiACS.cuh:113-157,216-256).
+//
+// Why it is exact.  A HARD metric needs few bits: every path metric lies within D = 12 units of the best
+// one and the best grows by at most 1 unit per stage, so between two renormalisations (32 stages) the
+// candidates of a stage stay within [-14, +47] units of the reference (vd_kernel_tg.h "Range").  With the
+// tagged scheme of the int32 patterns (TgFmt::INT: V = BASE + metric * 2^9 + 2^8 + h, 8-stage history
+// fields, |h| < 2^8) every value a stage computes lies in BASE + [-14 * 512, 48 * 512): with BASE = 16384,
+// in [9216, 40960), inside an unsigned 16-bit half.  Two chunks' metrics VA, VB sit in one 32-bit word
+// V = VB * 2^16 + VA, and a table entry holds both chunks' entries as m = EB * 2^16 + EA (signed halves).
+// 32-bit integer addition is a ring homomorphism: V + m = (VB + EB) * 2^16 + (VA + EA) exactly, and the
+// word's halves ARE VA + EA and VB + EB whenever both lie in [0, 2^16) -- which the bound guarantees for
+// every sum the kernel forms (the intermediate carries of two's-complement halves cancel modulo 2^32).
+// So one v_add_u32 / v_sub_u32 adds for both chunks, v_pk_max_u16 takes both maxima, and the DPP exchange
+// rides on the subtraction (v_sub_u32_dpp: the partner's V minus the shared entry).  A DPP stage is
+// v_add_u32 + v_sub_u32_dpp + v_pk_max_u16 for two chunk-states, an LDS-exchange stage v_sub_u32 +
+// v_add_u32 + v_pk_max_u16 with one crossbar round trip for both chunks; renormalisation is the int32
+// kernels' readfirstlane / s_sub / v_subrev on the whole word (again a homomorphism).
+//
+// The two chunks of a wave are consecutive chunks 2w, 2w+1 of the launch (the same batch: 6400 is even);
+// they decode in lockstep over the longer one's blocks, each emitting only its own words.  LDS per wave:
+// [guard | label-region table with the +tag area (TgTabLT<true>) | guard | ring A | ring B | guard]; two
+// rings in a wave's 5,120 B leave 6 slots each, so a traceback batch traces 5 words per chunk, both chunks'
+// words in one pass (lanes 0..4 chunk A, lanes 32..36 chunk B).
+#pragma once
+#include "vd_kernel_tg.h"
+
+namespace vd {
+
+// packed stages: V pinned to v60 like the other kernels
+template <int Q>
+__device__ __forceinline__ void pk_stage_dpp(uint32_t& V, uint32_t m)
+{
+    uint32_t a, b;
+#define VD_PK_DPP(CTRL)                                                                                      \
+    asm("v_add_u32 %1, %0, %3\n\ts_nop 0\n\tv_sub_u32_dpp %2, %0, %3 " CTRL " row_mask:0xf bank_mask:0xf\n\t" \
+        "v_pk_max_u16 %0, %1, %2"                                                                            \
+        : "+{v60}"(V), "=&v"(a), "=&v"(b) : "v"(m))
+    if constexpr (Q == 0) VD_PK_DPP("quad_perm:[1,0,3,2]");
+    else if constexpr (Q == 1) VD_PK_DPP("quad_perm:[2,3,0,1]");
+    else if constexpr (Q == 2) VD_PK_DPP("row_half_mirror");
+    else VD_PK_DPP("row_ror:8");
+#undef VD_PK_DPP
+}
+// LDS exchange, subtraction before the exchange (the partners share label and tag)
+template <bool X32>
+__device__ __forceinline__ void pk_stage_lds_pre(uint32_t& V, uint32_t m, int paddr)
+{
+    uint32_t a, b;
+    asm("v_sub_u32 %0, %1, %2" : "=v"(b) : "v"(V), "v"(m));
+    const uint32_t bp = X32 ? (uint32_t)__builtin_amdgcn_ds_bpermute(paddr, (int)b)
+                            : (uint32_t)__builtin_amdgcn_ds_swizzle((int)b, 0x401F);
+    asm("v_add_u32 %0, %1, %2" : "=v"(a) : "v"(V), "v"(m));
+    asm("v_pk_max_u16 %0, %1, %2" : "={v60}"(V) : "v"(a), "v"(bp));
+}
+// LDS exchange of V itself (M_B32's phase-0 stage: the partners' tag signs differ)
+__device__ __forceinline__ void pk_stage_lds_post(uint32_t& V, uint32_t m, int paddr)
+{
+    const uint32_t vp = (uint32_t)__builtin_amdgcn_ds_bpermute(paddr, (int)V);
+    uint32_t a, b;
+    asm("v_add_u32 %1, %0, %3\n\tv_sub_u32 %2, %4, %3\n\tv_pk_max_u16 %0, %1, %2"
+        : "+{v60}"(V), "=&v"(a), "=&v"(b) : "v"(m), "v"(vp));
+}
+
+// LDS layout of a wave (words)
+struct PkLds {
+    static constexpr int GW = kGuardWords;
+    static constexpr int TAB = TgTabLT<true>::BYTES / 4;
+    static constexpr int TBS = (kWaveLdsWords - 3 * GW - TAB) / 128 - 1;  // words per traceback batch and chunk
+    static constexpr int RING = (TBS + 1) * 64;                            // words per chunk ring
+    static constexpr int TAB_OFF = GW, RING_OFF = 2 * GW + TAB;
+    static constexpr int WAVE = 3 * GW + TAB + 2 * RING;
+    static __device__ __forceinline__ int guard(int i) { return i < GW ? i : i < 2 * GW ? TAB + i : TAB + 2 * RING + i; }
+};
+static_assert(PkLds::TBS == 5 && kWaves * PkLds::WAVE * 4 <= 20480, "8 workgroups of 4 waves per CU");
+
+template <int CORE>
+__global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(8))) void vd_decode_pk(const void* __restrict__ in_all, void* __restrict__ out_all, Geom geo)
+{
+    using IN = TgIn<HARD>;
+    using TT = TgTabLT<true>;
+    using LL = PkLds;
+    constexpr int J = 8, S = 9;
+    constexpr bool ALT = CORE == B32;  // M_B32: the upper position half takes the +tag entries at phase 0
+    __shared__ __attribute__((aligned(16))) uint32_t lds[kWaves * LL::WAVE];
+    const int lane = threadIdx.x & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int pos = tg_pos(lane);
+    uint32_t* const wlds = lds + wv * LL::WAVE;
+    char* const tabb = (char*)(wlds + LL::TAB_OFF);
+    uint32_t* const ringA = wlds + LL::RING_OFF;
+    uint32_t* const ringB = ringA + LL::RING;
+    // chunks 2w, 2w+1 of the launch (batch b: launch chunks b * nchunks ..; nchunks is even)
+    const uint32_t gc = 2u * (blockIdx.x * kWaves + (uint32_t)wv);
+    const uint32_t batch = gc / geo.nchunks;
+    const uint32_t cA = gc - batch * geo.nchunks;
+    const void* const in = (const char*)in_all + batch * geo.inStride;
+    uint32_t* const out = (uint32_t*)((char*)out_all + batch * geo.outStride);
+    const ChunkRange crA = chunk_range(geo, cA), crB = chunk_range(geo, cA + 1);
+    if (crA.words == 0 && crB.words == 0) return;
+    if (geo.check && lane < 3 * kGuardWords) wlds[LL::guard(lane)] = kGuardPattern;
+
+    // per-lane LDS byte offsets of this position's entries per phase (vd_decode_tg's INT table)
+    const bool upper5 = (pos >> 5) & 1;
+    int aK[6];
+    constexpr int LSTR = TT::REGION;
+    sfor<6>([&](auto KK) {
+        constexpr int K = decltype(KK)::value;
+        aK[K] = LSTR * own_label(pos, K);
+    });
+    if constexpr (ALT) aK[0] = upper5 ? TT::ALT_OFF + 8 * own_label(pos, 0) : aK[0];
+    const int pa5 = 4 * (lane ^ 32);
+    // table-build roles (as vd_decode_tg): lane l builds table index l (stage sA), lanes 0..31 also 64 + l (sB)
+    const int sA = TgTabL::stage(lane), sB = TgTabL::stage(64 + (lane & 31));
+    const int tagA = 1 << (sA % J), tagB = 1 << (sB % J);
+    // entry tag of the row's own class, both halves: tg0 * 65537 (M_FP16: own wins ties, +2^j; else -2^j)
+    const int32_t tg0A = (CORE == F16 ? tagA : -tagA) * 65537, tg0B = (CORE == F16 ? tagB : -tagB) * 65537;
+    const uint32_t tabl = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)tabb;
+    constexpr uint32_t BASE = 16384;
+    constexpr uint32_t VB1 = BASE + (1u << (S - 1));  // a half with metric 0 and a cleared field
+    constexpr uint32_t VBASE = VB1 * 65537u;
+    constexpr uint32_t FNM = 0xFE00FE00u, FHF = 0x01000100u;  // field clear: (V & FNM) | FHF, both halves
+    Fair fair;
+    fair.begin(batch + 1 < geo.nbatch ? nullptr : geo.fair, lane);
+    const uint64_t availB = IN::bytes(geo.availStages);
+    const uint32_t vo1 = IN::voff(sA), vo2 = IN::voff(sB);
+    const uint32_t WA = crA.words, WB = crB.words, nblk = (WA > WB ? WA : WB) + 2;
+    const uint64_t startA = crA.startWord * 32ull, startB = crB.startWord * 32ull;
+    uint32_t V = VBASE;
+    uint32_t kb = 0;
+    uint32_t tbn = LL::TBS - (blockIdx.x & 3u);  // staggered first traceback batches
+    __amdgpu_buffer_rsrc_t rsA = tg_rsrc<HARD>(in, startA, availB), rsB = tg_rsrc<HARD>(in, startB, availB);
+    uint32_t rAA = IN::template load<0>(rsA, vo1), rBA = IN::template load<0>(rsA, vo2);
+    uint32_t rAB = IN::template load<0>(rsB, vo1), rBB = IN::template load<0>(rsB, vo2);
+    // traceback roles: lanes 0..31 trace chunk A's words, 32..63 chunk B's
+    const bool tbB = lane >= 32;
+    const uint32_t tbl = (uint32_t)(lane & 31);
+    const char* const tbring = (const char*)(tbB ? ringB : ringA);
+    uint32_t* const tbout = out + (tbB ? crB.startWord : crA.startWord);
+    const uint32_t tbW = tbB ? WB : WA;
+
+    typedef uint32_t u2v __attribute__((ext_vector_type(2)));
+    typedef __attribute__((address_space(3))) const volatile u2v* lptr;
+    const __attribute__((address_space(3))) char* tl = (const __attribute__((address_space(3))) char*)tabb;
+    constexpr int TGD = 4;
+    u2v vp[96];
+    auto issue = [&](auto Rc) {
+        constexpr int r = decltype(Rc)::value;
+        constexpr int K = r % 6;
+        if constexpr ((r / 6) % 2 == 0) vp[r] = *(lptr)(tl + aK[K] + TT::row(r));
+    };
+    auto block = [&](auto PHc, uint32_t j) {
+        constexpr int PH = decltype(PHc)::value;
+        constexpr int BB = PH / 2;
+        uint32_t wA = 0, wB = 0;
+        sfor<32>([&](auto I) {
+            constexpr int i = decltype(I)::value;
+            constexpr int K = (PH + i) % 6;
+            constexpr int Q = (K + 5) % 6;
+            constexpr int r = 32 * BB + i;
+            constexpr bool ODD = (r / 6) % 2 == 1;
+            constexpr int RP = ODD ? r - 6 : r;
+            const uint32_t m = ODD ? vp[RP].y : vp[RP].x;
+            if constexpr (Q <= 3) pk_stage_dpp<Q>(V, m);
+            else if constexpr (Q == 4) pk_stage_lds_pre<false>(V, m, pa5);
+            else if constexpr (ALT) pk_stage_lds_post(V, m, pa5);
+            else pk_stage_lds_pre<true>(V, m, pa5);
+            if constexpr (r + TGD < 96) issue(std::integral_constant<int, r + TGD>{});
+            if constexpr (i % J == J - 1) {
+                // field read-out, both chunks: bits 1..8 of each half into byte g of its ring word (SDWA), then
+                // both fields cleared; at the block end the renormalisation on the whole word (vd_decode_tg)
+                constexpr int g = (i % 32) / J;
+                uint32_t sr;
+#define VD_PK_RO(SEL, UNUSED)                                                                                \
+    "v_lshrrev_b32_sdwa %[wa], 1, %[V] dst_sel:" SEL " dst_unused:" UNUSED " src0_sel:DWORD src1_sel:DWORD\n\t"  \
+    "v_lshrrev_b32_sdwa %[wb], 1, %[V] dst_sel:" SEL " dst_unused:" UNUSED " src0_sel:DWORD src1_sel:WORD_1\n\t" \
+    "v_and_or_b32 %[V], %[V], %[fnm], %[fhf]"
+#define VD_PK_RN "\n\ts_nop 0\n\tv_readfirstlane_b32 %[sr], %[V]\n\ts_sub_u32 %[sr], %[sr], %[vb]\n\tv_subrev_u32 %[V], %[sr], %[V]"
+#define VD_PK_IN [fnm] "v"(FNM), [fhf] "s"(FHF), [vb] "n"(VBASE)
+                if constexpr (g == 0)
+                    asm(VD_PK_RO("BYTE_0", "UNUSED_PAD") : [V] "+{v60}"(V), [wa] "=&v"(wA), [wb] "=&v"(wB) : VD_PK_IN);
+                else if constexpr (g == 1)
+                    asm(VD_PK_RO("BYTE_1", "UNUSED_PRESERVE") : [V] "+{v60}"(V), [wa] "+v"(wA), [wb] "+v"(wB) : VD_PK_IN);
+                else if constexpr (g == 2)
+                    asm(VD_PK_RO("BYTE_2", "UNUSED_PRESERVE") : [V] "+{v60}"(V), [wa] "+v"(wA), [wb] "+v"(wB) : VD_PK_IN);
+                else
+                    asm(VD_PK_RO("BYTE_3", "UNUSED_PRESERVE") VD_PK_RN
+                        : [V] "+{v60}"(V), [wa] "+v"(wA), [wb] "+v"(wB), [sr] "=&s"(sr) : VD_PK_IN : "scc");
+#undef VD_PK_IN
+#undef VD_PK_RN
+#undef VD_PK_RO
+            }
+        });
+        if constexpr (CORE == F16) {
+            wA = ~wA;
+            wB = ~wB;
+        }
+        wave_sync();
+        if (j >= 1) {
+            ringA[(j - 1 - kb) * 64 + pos] = wA;
+            ringB[(j - 1 - kb) * 64 + pos] = wB;
+        }
+        if (j >= 2 && (j - 1 - kb == tbn || j == nblk - 1)) {
+            wave_sync();
+            const uint32_t nw = j - 1 - kb;
+            const uint32_t k = kb + tbl;
+            if (tbl < nw && k < tbW) {
+                const TbC tc = tb_direct<J, CORE == B32>((int)k);
+                tbout[k] = traceback_word_tg<J, CORE == B32>(tbring, (tbl + 1u) * 256u, tc);
+            }
+            wave_sync();
+            ringA[pos] = wA;  // block j becomes slot 0 of the next batch
+            ringB[pos] = wB;
+            kb = j - 1;
+            tbn = LL::TBS;
+        }
+        return j + 1 < nblk;
+    };
+    // the four entries of a stage for both chunks: E[L] = BM[L] * 2^S + tg0 per half (TgFmt::INT's table),
+    // from (A, B) = (BM[3], BM[2]) of each chunk packed as A_A + A_B * 2^16 (signed halves, |.| <= 1: an i24)
+    auto put_row = [&](auto PT, uint32_t wa, uint32_t wb, int li, int K) {
+        constexpr int part = decltype(PT)::value;
+        const int32_t tg = part ? tg0B : tg0A;
+        int AA, BA, AB, BBv;
+        IN::ab(wa, li, AA, BA, 1.0f);
+        IN::ab(wb, li, AB, BBv, 1.0f);
+        const int32_t pa = AA + AB * 65536, pb = BA + BBv * 65536;
+        auto f = [](int32_t x) { return __builtin_bit_cast(float, x); };
+        const int32_t e3 = __mul24(pa, 1 << S) + tg, e2 = __mul24(pb, 1 << S) + tg;
+        const int32_t e0 = __mul24(pa, -(1 << S)) + tg, e1 = __mul24(pb, -(1 << S)) + tg;
+        lds_write_addtid4<256 * part, TT::REGION>(tabl, f(e0), f(e1), f(e2), f(e3));
+        if (ALT && K == 0) {  // phase-0 lanes: the +tag entries E+[L] = BM[L] * 2^S - tg0 (ALT area)
+            const int32_t d = -2 * tg;
+            lds_write_addtid4<TT::ALT_OFF + 256 * part, 8>(tabl, f(e0 + d), f(e1 + d), f(e2 + d), f(e3 + d));
+        }
+    };
+    const int r6a = sA % 6, r6b = sB % 6;
+    using P0 = std::integral_constant<int, 0>;
+    using P1 = std::integral_constant<int, 1>;
+    for (uint32_t j = 0;; j += 3) {
+        put_row(P0{}, rAA, rAB, sA, r6a);
+        if (lane < 32) put_row(P1{}, rBA, rBB, sB, r6b);
+        rsA = tg_rsrc<HARD>(in, startA + 32ull * (j + 3), availB);
+        rsB = tg_rsrc<HARD>(in, startB + 32ull * (j + 3), availB);
+        rAA = IN::template load<0>(rsA, vo1);
+        rBA = IN::template load<0>(rsA, vo2);
+        rAB = IN::template load<0>(rsB, vo1);
+        rBB = IN::template load<0>(rsB, vo2);
+        if ((j / 3) % 2 == 0) fair.group(j, 3u, lane);
+        wave_sync();
+        sfor<TGD>([&](auto X) { issue(X); });
+        if (!block(std::integral_constant<int, 0>{}, j)) break;
+        if (!block(std::integral_constant<int, 2>{}, j + 1)) break;
+        if (!block(std::integral_constant<int, 4>{}, j + 2)) break;
+        wave_sync();
+    }
+    fair.end(lane);
+    if (geo.check) {
+        wave_sync();
+        const bool bad = lane < 3 * kGuardWords && wlds[LL::guard(lane)] != kGuardPattern;
+        const uint32_t nbad = (uint32_t)__builtin_popcountll(__ballot(bad));
+        if (lane == 0 && nbad) atomicAdd(geo.check, nbad);
+    }
+}
+
+}  // namespace vd

@@ -1,0 +1,63 @@
+"""Batched HARD launches on vd_decode_pk (vd_kernel_pk.h): two chunks per wave, one in each 16-bit half of
+the metric word.  Every batch must equal the oracle word for word and the fp32 tagged kernel's output
+(VD_NO_PK=1 at decoder creation selects it), for every metric core's tie rule, including chunk counts where
+the two chunks of a wave differ in length (an odd number of long chunks), partitions with empty chunks, and
+saturated inputs (SNR 15: the best path gains every stage, the largest range the int16 halves must hold)."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from vitdec import HARD, M_B16, M_B32, M_FP16
+from test_gpu_parity import name
+
+
+def _batches(gpu, opt, nbits, snr, nb, seed):
+    n = 2 * nbits
+    nin = gpu.lib().vd_input_size(opt, n)
+    stride = (nin + 255) // 256 * 256
+    packed = torch.zeros(nb * stride, dtype=torch.uint8, device="cuda")
+    bits = torch.empty(nbits, dtype=torch.uint8, device="cuda")
+    for b in range(nb):
+        gpu.simulate_device(opt, nbits, snr, seed + 2 * b, seed + 1 + 2 * b, bits.data_ptr(), packed.data_ptr() + b * stride)
+    torch.cuda.synchronize()
+    return packed, stride, nin
+
+
+def _decode_batched(gpu, opt, packed, stride, n, nb, no_pk):
+    nout = gpu.lib().vd_output_size(opt, n)
+    ostride = (nout + 255) // 256 * 256
+    out = torch.full((nb * ostride,), 0x5A, dtype=torch.uint8, device="cuda")
+    old = os.environ.get("VD_NO_PK")
+    os.environ["VD_NO_PK"] = "1" if no_pk else "0"
+    try:
+        with gpu.ViterbiCUDA(opt) as dec:
+            dec.run_device_batch(packed.data_ptr(), stride, out.data_ptr(), ostride, n, nb)
+            torch.cuda.synchronize()
+    finally:
+        if old is None:
+            del os.environ["VD_NO_PK"]
+        else:
+            os.environ["VD_NO_PK"] = old
+    for b in range(nb):  # nothing written between the batches' outputs
+        assert bool((out[b * ostride + nout:(b + 1) * ostride] == 0x5A).all())
+    return out, ostride, nout
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("opt", [HARD | M_B32, HARD | M_B16, HARD | M_FP16], ids=name)
+@pytest.mark.parametrize("nbits,snr", [(1_000_032, 0.5), (4_000_032, 1.2), (150_000, 0.0), (2_000_000, 15.0)])
+def test_packed_batches_equal_oracle_and_fp32_kernel(gpu, vo, opt, nbits, snr):
+    nb, n = 3, 2 * nbits
+    pack = (nbits - 64) // 32
+    packed, stride, nin = _batches(gpu, opt, nbits, snr, nb, 71)
+    pk, ostride, nout = _decode_batched(gpu, opt, packed, stride, n, nb, no_pk=False)
+    tg, _, _ = _decode_batched(gpu, opt, packed, stride, n, nb, no_pk=True)
+    for b in range(nb):
+        p = packed[b * stride:b * stride + nin].cpu().numpy().view(np.int32)
+        ref, ok = vo.decode(opt, p, input_num=n, nthreads=16)
+        got = pk[b * ostride:b * ostride + nout].cpu().numpy().view(ref.dtype)
+        bad = np.flatnonzero(got != ref)
+        assert bad.size == 0, f"batch {b}: {bad.size} of {ref.size} words differ (pack {pack}, rem {pack % 6400}), first {bad[:5]}"
+        assert torch.equal(pk[b * ostride:b * ostride + nout], tg[b * ostride:b * ostride + nout])

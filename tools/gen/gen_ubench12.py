@@ -13,7 +13,9 @@ OPS = {"add_f32": "v_add_f32 {d}, {d}, v40", "sub_f32": "v_sub_f32 {d}, {d}, v40
        "max_i32_dpp": "v_max_i32_dpp {d}, {d}, v40 " + QP, "sub_u32_dpp": "v_sub_u32_dpp {d}, {d}, v40 " + QP,
        "and_or_b32": "v_and_or_b32 {d}, {d}, v40, v41",
        "lshr_sdwa": "v_lshrrev_b32_sdwa {d}, 1, {d} dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD",
-       "bfe_u32": "v_bfe_u32 {d}, {d}, 1, 8", "cvt_f32_i32": "v_cvt_f32_i32 {d}, {d}"}
+       "bfe_u32": "v_bfe_u32 {d}, {d}, 1, 8", "cvt_f32_i32": "v_cvt_f32_i32 {d}, {d}",
+       "add3_u32": "v_add3_u32 {d}, {d}, v40, v41", "pk_max_u16": "v_pk_max_u16 {d}, {d}, v40",
+       "pk_max_i16": "v_pk_max_i16 {d}, {d}, v40", "pk_add_u16": "v_pk_add_u16 {d}, {d}, v40"}
 PK = {"pk_add_f32": "v_pk_add_f32 v[{a}:{b}], v[{a}:{b}], v[40:41]",
       "pk_fma_f32": "v_pk_fma_f32 v[{a}:{b}], v[{a}:{b}], v[40:41], v[40:41]",
       "permlane32_swap": "v_permlane32_swap_b32 v{a}, v{b}", "permlane16_swap": "v_permlane16_swap_b32 v{a}, v{b}"}
@@ -54,6 +56,14 @@ def stage(kind, nch=1, stages=24):
                         f"v_pk_max_i16 {V}, {t1}, {t2}"]
             elif kind == "pk16 plain (2 chunks)":  # partner value from elsewhere (LDS): pk add / sub / max
                 out += [f"v_pk_add_i16 {t1}, {V}, v40", f"v_pk_sub_i16 {t2}, v41, v40", f"v_pk_max_i16 {V}, {t1}, {t2}"]
+            elif kind == "pk32 dpp (2 chunks)":  # two int16 metrics per lane, 32-bit adds that never carry across
+                out += [f"v_add3_u32 {t1}, {V}, v40, v41", "s_nop 0", f"v_sub_u32_dpp {t2}, {V}, v40 {QP}",
+                        f"v_pk_max_u16 {V}, {t1}, {t2}"]
+            elif kind == "pk32 plain (2 chunks)":  # partner value from elsewhere (LDS)
+                out += [f"v_add3_u32 {t1}, {V}, v40, v41", f"v_sub_u32 {t2}, v41, v40", f"v_pk_max_u16 {V}, {t1}, {t2}"]
+            elif kind == "pk32 dpp add (2 chunks)":  # cost reference: v_add_u32 in place of v_add3_u32
+                out += [f"v_add_u32 {t1}, {V}, v40", "s_nop 0", f"v_sub_u32_dpp {t2}, {V}, v40 {QP}",
+                        f"v_pk_max_u16 {V}, {t1}, {t2}"]
             elif kind == "add+max f32 (no exchange)":
                 out += [f"v_add_f32 {t1}, {V}, v40", f"v_sub_f32 {t2}, {V}, v40", f"v_max_f32 {V}, {t1}, {t2}"]
     return out
@@ -64,7 +74,8 @@ V += [(op, [PK[op].format(a=10 + 2 * (i % 8), b=11 + 2 * (i % 8)) for i in range
 for k in ["3op f32", "2op f32", "3op i32", "2op i32", "swap f32", "add+max f32 (no exchange)"]:
     V.append((f"stage {k}", stage(k), 24))
     V.append((f"stage {k} x2 chains", stage(k, 2), 48))
-for k in ["pk16 dpp (2 chunks)", "pk16 plain (2 chunks)"]:
+for k in ["pk16 dpp (2 chunks)", "pk16 plain (2 chunks)", "pk32 dpp (2 chunks)", "pk32 plain (2 chunks)",
+          "pk32 dpp add (2 chunks)"]:
     V.append((f"stage {k} per 2 states", stage(k), 24))
     V.append((f"stage {k} x2 chains per 2 states", stage(k, 2), 48))
 for k in ["2op pk f32 (pair)", "3op pk f32 (pair)", "inlane pk (pair)"]:

@@ -13,7 +13,7 @@
 #include <random>
 #include <vector>
 #include <algorithm>
-#include "../gpu-accelerated-viterbi-decoder_amd/csrc/vd_kernel_tg.h"
+#include "../gpu-accelerated-viterbi-decoder_amd/csrc/vd_kernel_pk.h"
 #include "../gpu-accelerated-viterbi-decoder_amd/csrc/vd_segplan.h"
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP error %s at %d\n", hipGetErrorString(e), __LINE__); exit(1); } } while (0)
 using KFn = void (*)(const void*, void*, vd::Geom);
@@ -24,13 +24,12 @@ struct V {
     static constexpr KFn soft8 = (KFn)vd::vd_decode_tg<vd::SOFT8, vd::B16, 32, ABL>;
 };
 // a variant: kernels, and the segment table (vd_segplan.h SegMode) + warm-up blocks of its segment launches
-struct Variant { const char* name; KFn hard, soft8; int seg = vd::kSegPieces; uint32_t warm = vd::kSplitWarm; };
+struct Variant { const char* name; KFn hard, soft8; int seg = vd::kSegPieces; uint32_t warm = vd::kSplitWarm; KFn hardBatched = nullptr; };
 #ifndef VD_ABX_VARIANTS
 #define VD_ABX_VARIANTS                                                                                      \
-    {"product", V<0>::hard, V<0>::soft8},                                                                    \
-    {"table reads 8 stages ahead", V<vd::kAblTgd8>::hard, V<vd::kAblTgd8>::soft8},                           \
-    {"fairness every 4th group head", V<vd::kAblFair4>::hard, V<vd::kAblFair4>::soft8},                      \
-    {"no fairness controller", V<vd::kAblNoFair>::hard, V<vd::kAblNoFair>::soft8},
+    {"fp32 tagged core (vd_decode_tg)", V<0>::hard, V<0>::soft8},                                           \
+    {"batched hard: two chunks per wave (vd_decode_pk)", V<0>::hard, V<0>::soft8, vd::kSegPieces, vd::kSplitWarm, \
+     (KFn)vd::vd_decode_pk<vd::B32>},
 #endif
 
 static double median(std::vector<float> v)
@@ -113,7 +112,8 @@ int main(int argc, char** argv)
             gh.inStride = strH;
             gS.inStride = strS;
             CK(hipEventRecord(ev[0]));
-            hipLaunchKernelGGL(vs[v].hard, dim3(gridB), dim3(256), 0, 0, bH, bO, gh);
+            if (vs[v].hardBatched) hipLaunchKernelGGL(vs[v].hardBatched, dim3(gridB / 2), dim3(256), 0, 0, bH, bO, gh);
+            else hipLaunchKernelGGL(vs[v].hard, dim3(gridB), dim3(256), 0, 0, bH, bO, gh);
             CK(hipEventRecord(ev[1]));
             hipLaunchKernelGGL(vs[v].soft8, dim3(gridB), dim3(256), 0, 0, bS, bO, gS);
             CK(hipEventRecord(ev[2]));
@@ -145,7 +145,8 @@ int main(int argc, char** argv)
                 CK(hipMemset(bO, 0, ostr * K));
                 KFn f = w ? vs[v].soft8 : vs[v].hard;
                 const char* in = w ? bS : bH;
-                if (kind == 0) hipLaunchKernelGGL(f, dim3(gridB), dim3(256), 0, 0, in, bO, gg);
+                if (kind == 0 && w == 0 && vs[v].hardBatched) hipLaunchKernelGGL(vs[v].hardBatched, dim3(gridB / 2), dim3(256), 0, 0, in, bO, gg);
+                else if (kind == 0) hipLaunchKernelGGL(f, dim3(gridB), dim3(256), 0, 0, in, bO, gg);
                 else hipLaunchKernelGGL(f, dim3(gridS), dim3(256), 0, 0, in, bO + (K - 1) * ostr, gg);
                 CK(hipDeviceSynchronize());
                 CK(hipMemcpy(v ? got.data() : ref.data(), bO + (K - 1) * ostr, g.packNum * 4, hipMemcpyDeviceToHost));
