@@ -33,7 +33,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md)
 SNR_DB = 2.0
 WARM_S = 0.5      # minimum warm-up (seconds of steps) before the timed region
 POOL = 128        # at most this many resident batches per workload (128 SOFT8 batches: 8.2 GB of input)
-PMC_ROUND = "r03"  # profiles/<round>/pmc_summary.json, profiles/<round>/ablate_batched.log
+PMC_ROUND = "r04"  # profiles/<round>/pmc_summary.json, profiles/<round>/ablate_batched.log
 
 WORKLOADS = [
     ("hard_b32", vitdec.HARD | vitdec.M_B32 | vitdec.O_B32),
@@ -157,7 +157,8 @@ def acs_only_ms(name):
     only the ACS recursion left (tools/vd_ablate 'ACS only' variant: no table build/reads, read-out,
     loads or traceback; 8 batches per launch as the bench launches them), from the committed ablation log
     of this round; None if absent."""
-    key = {"hard_b32": "tg hard/b32 ACS only ", "soft8_b16": "tg soft8/b16 ACS only "}.get(name)
+    # (the batched HARD launches run vd_decode_pk since round 4: no ablation of that kernel, no ceiling)
+    key = {"soft8_b16": "tg soft8/b16 ACS only "}.get(name)
     p = os.path.join(ROOT, "profiles", PMC_ROUND, "ablate_batched.log")
     if key is None or not os.path.exists(p):
         return None
@@ -186,10 +187,12 @@ def valu_view(pmc, kernel_ms, stages, name, msg_bits):
     if not c or "SQ_INSTS_VALU" not in c:
         return None
     insts = c["SQ_INSTS_VALU"]
-    v = {"insts_per_launch": round(insts), "insts_per_wave_stage": round(insts / stages, 3),
-         "wave_stages_per_launch": stages}
+    # per chunk-stage (one chunk's 64 states for one stage): a wave-stage of vd_decode_tg; vd_decode_pk (batched
+    # HARD) decodes two chunks per wave, so its wave-stages are half its chunk-stages
+    v = {"insts_per_launch": round(insts), "insts_per_chunk_stage": round(insts / stages, 3),
+         "chunk_stages_per_launch": stages}
     if "SQ_INSTS_LDS" in c:
-        v["lds_insts_per_wave_stage"] = round(c["SQ_INSTS_LDS"] / stages, 3)
+        v["lds_insts_per_chunk_stage"] = round(c["SQ_INSTS_LDS"] / stages, 3)
     if "GRBM_GUI_ACTIVE" in c:
         cyc = c["GRBM_GUI_ACTIVE"] / N_XCD
         v["issue_pct"] = round(100.0 * insts * 2 / (N_SIMD * cyc), 1)
@@ -741,7 +744,7 @@ def main():
     if checks is not None:
         for b in batches:
             for k in sorted({0, P - 1}):
-                nin = b["inp"].numel()
+                nin = 4 * b["input_num"] if b["llr"] else b["inp"].numel()  # float channel values / packed words
                 checks.append((f"{b['name']}[batch {k}]", b["opt"],
                                b["inps"][k * b["istride"]:k * b["istride"] + nin].cpu().numpy(),
                                b["outs"][k * b["ostride"]:k * b["ostride"] + b["nout"]].cpu().numpy(), b["input_num"],
