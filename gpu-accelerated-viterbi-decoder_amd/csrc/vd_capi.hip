@@ -119,17 +119,27 @@ launch_fn pick_ob(int ob)
     return ob == 1 ? &launch_t<CH, CORE, 16> : &launch_t<CH, CORE, 32>;
 }
 
-// batched HARD / 32-bit-output launches: two chunks per wave in int16 halves (vd_kernel_pk.h)
-template <int CORE>
+// batched HARD / SOFT4 / FP32 launches with 32-bit output words: two chunks per wave in int16 halves
+// (vd_kernel_pk.h)
+template <int CH, int CORE>
 void launch_pk(const void* in, void* out, vd::Geom g, unsigned grid, hipStream_t s)
 {
-    hipLaunchKernelGGL((vd::vd_decode_pk<CORE>), dim3(grid), dim3(64 * vd::kWaves), 0, s, in, out, g);
+    hipLaunchKernelGGL((vd::vd_decode_pk<CH, CORE>), dim3(grid), dim3(64 * vd::kWaves), 0, s, in, out, g);
+}
+template <int CH>
+launch_fn pick_pk_core(int me)
+{
+    return me == 0 ? &launch_pk<CH, 0> : me == 1 ? &launch_pk<CH, 1> : &launch_pk<CH, 2>;
 }
 launch_fn pick_pk(int o)
 {
-    if (ch_of(o) != 0 || out_of(o) != 0) return nullptr;
-    const int me = met_of(o);
-    return me == 0 ? &launch_pk<0> : me == 1 ? &launch_pk<1> : &launch_pk<2>;
+    if (out_of(o) != 0) return nullptr;
+    switch (ch_of(o)) {
+    case 0: return pick_pk_core<vd::HARD>(met_of(o));
+    case 1: return pick_pk_core<vd::SOFT4>(met_of(o));
+    case 4: return pick_pk_core<vd::FP32>(met_of(o));
+    }
+    return nullptr;
 }
 
 template <int L>
@@ -150,23 +160,32 @@ launch_fn pick(int o, bool llr)
     return llr ? pick_ch<vd::kLlr>(o) : pick_ch<0>(o);
 }
 
-// CORE names the option's tie rule; every kernel computes on the fp32 exact-integer tagged core (SOFT16:
-// int32 patterns), none on packed int16 / fp16 arithmetic
+// CORE names the option's tie rule.  vd_decode_tg computes on the fp32 exact-integer tagged core (SOFT16:
+// int32 patterns); vd_decode_pk (batched HARD / SOFT4 / FP32) on exact-integer tagged int16 halves, two
+// chunks per lane; none on fp16 arithmetic
 const char* kname(int o)
 {
     static const char* names[5][3] = {
-        {"vd_decode_pk<B32> (batched: two chunks per lane in int16 halves) / vd_decode_tg<HARD,B32> (single batch: "
+        {"vd_decode_pk<HARD,B32> (batched: two chunks per lane in int16 halves) / vd_decode_tg<HARD,B32> (single batch: "
          "fp32 tagged core); M_B32 tie rule",
-         "vd_decode_pk<B16> (batched: two chunks per lane in int16 halves) / vd_decode_tg<HARD,B16> (single batch: "
+         "vd_decode_pk<HARD,B16> (batched: two chunks per lane in int16 halves) / vd_decode_tg<HARD,B16> (single batch: "
          "fp32 tagged core); M_B16 tie rule",
-         "vd_decode_pk<F16> (batched: two chunks per lane in int16 halves) / vd_decode_tg<HARD,F16> (single batch: "
+         "vd_decode_pk<HARD,F16> (batched: two chunks per lane in int16 halves) / vd_decode_tg<HARD,F16> (single batch: "
          "fp32 tagged core); M_FP16 tie rule"},
-        {"vd_decode_tg<SOFT4,B32> (fp32 tagged core, M_B32 tie rule)", "vd_decode_tg<SOFT4,B16> (fp32 tagged core, M_B16 tie rule)",
-         "vd_decode_tg<SOFT4,F16> (fp32 tagged core, M_FP16 tie rule)"},
+        {"vd_decode_pk<SOFT4,B32> (batched: two chunks per lane in int16 halves) / vd_decode_tg<SOFT4,B32> (single "
+         "batch: fp32 tagged core); M_B32 tie rule",
+         "vd_decode_pk<SOFT4,B16> (batched: two chunks per lane in int16 halves) / vd_decode_tg<SOFT4,B16> (single "
+         "batch: fp32 tagged core); M_B16 tie rule",
+         "vd_decode_pk<SOFT4,F16> (batched: two chunks per lane in int16 halves) / vd_decode_tg<SOFT4,F16> (single "
+         "batch: fp32 tagged core); M_FP16 tie rule"},
         {"vd_decode_tg<SOFT8,B32> (fp32 tagged core, M_B32 tie rule)", "vd_decode_tg<SOFT8,B16> (fp32 tagged core, M_B16 tie rule)", "-"},
         {"vd_decode_tg<SOFT16,B32> (int32 tagged patterns, M_B32 tie rule)", "-", "-"},
-        {"vd_decode_tg<FP32,B32> (fp32 tagged core, M_B32 tie rule)", "vd_decode_tg<FP32,B16> (fp32 tagged core, M_B16 tie rule)",
-         "vd_decode_tg<FP32,F16> (fp32 tagged core, M_FP16 tie rule)"},
+        {"vd_decode_pk<FP32,B32> (batched: two chunks per lane in int16 halves) / vd_decode_tg<FP32,B32> (single "
+         "batch: fp32 tagged core); M_B32 tie rule",
+         "vd_decode_pk<FP32,B16> (batched: two chunks per lane in int16 halves) / vd_decode_tg<FP32,B16> (single "
+         "batch: fp32 tagged core); M_B16 tie rule",
+         "vd_decode_pk<FP32,F16> (batched: two chunks per lane in int16 halves) / vd_decode_tg<FP32,F16> (single "
+         "batch: fp32 tagged core); M_FP16 tie rule"},
     };
     if (!valid(o)) return "-";
     return names[ch_of(o)][met_of(o)];
@@ -204,7 +223,8 @@ struct vd_decoder {
     hipStream_t s_in = nullptr, s_out = nullptr;
     DeviceState* ds = nullptr;  // the device's board / segment tables (looked up once, vd_create)
     int split = 1;              // segment launches: 0 none (VD_NO_SPLIT=1), 1 pieces, 2 thirds, 3 sevenths (VD_SPLIT=...)
-    int pk = 1;                 // batched HARD launches on vd_decode_pk (VD_NO_PK=1: on vd_decode_tg)
+    int pk = 1;                 // batched HARD/SOFT4/FP32 launches on vd_decode_pk (VD_NO_PK=1: on vd_decode_tg)
+    int pk1 = 0;                // single-batch launches on vd_decode_pk too (VD_PK_SINGLE=1; study)
     uint32_t* check = nullptr;  // LDS guard violation counter (vd_set_guard_check), null = off
 };
 
@@ -318,7 +338,7 @@ static int launch_decode(const vd_decoder* d, const void* in_d, void* out_d, siz
     g.nbatch = nbatch;
     g.inStride = inStride;
     g.outStride = outStride;
-    launch_fn fp = nbatch > 1 && !llr && d->pk && g.nchunks % (2 * vd::kWaves) == 0 ? pick_pk(options) : nullptr;
+    launch_fn fp = (nbatch > 1 || d->pk1) && !llr && d->pk && g.nchunks % (2 * vd::kWaves) == 0 ? pick_pk(options) : nullptr;
     if (fp) {  // two chunks per wave: nchunks * nbatch / 8 workgroups
         fp(in_d, out_d, g, (unsigned)((uint64_t)g.nchunks * nbatch / (2 * vd::kWaves)), s);
         VD_HIP(hipGetLastError());
@@ -380,6 +400,8 @@ int vd_create(int options, size_t preallocInputNum, int device, vd_decoder** out
     d->split = nosplit && nosplit[0] == '1' ? 0 : smode && !strcmp(smode, "thirds") ? 2 : smode && !strcmp(smode, "sevenths") ? 3 : 1;
     const char* nopk = std::getenv("VD_NO_PK");
     d->pk = nopk && nopk[0] == '1' ? 0 : 1;
+    const char* pk1 = std::getenv("VD_PK_SINGLE");
+    d->pk1 = pk1 && pk1[0] == '1' ? 1 : 0;
     const char* chk = std::getenv("VD_CHECK");
     if (chk && chk[0] == '1') {
         int rc = vd_set_guard_check(d, 1);

@@ -1,6 +1,6 @@
-// vd_kernel_pk.h -- vd_decode_pk<CORE>: HARD input, TWO chunks per wave, one in each 16-bit half of the
-// lane's metric word (batched launches).  Same decode as vd_decode_tg<HARD, CORE, 32> word for word
-// (reference viterbi_core, src/viterbi/viterbi.cu:144-207; tie rules viterbiACS.cuh:113-157,216-256).
+// vd_kernel_pk.h -- vd_decode_pk<CH, CORE>: HARD, SOFT4 or FP32 input, TWO chunks per wave, one in each
+// 16-bit half of the lane's metric word (batched launches).  Same decode as vd_decode_tg<CH, CORE, 32> word
+// for word (reference viterbi_core, src/viterbi/viterbi.cu:144-207; tie rules viterbiACS.cuh:113-157,216-256).
 //
 // Why it is exact.  A HARD metric needs few bits: every path metric lies within D = 12 units of the best
 // one and the best grows by at most 1 unit per stage, so between two renormalisations (32 stages) the
@@ -12,6 +12,9 @@
 // 32-bit integer addition is a ring homomorphism: V + m = (VB + EB) * 2^16 + (VA + EA) exactly, and the
 // word's halves ARE VA + EA and VB + EB whenever both lie in [0, 2^16) -- which the bound guarantees for
 // every sum the kernel forms (the intermediate carries of two's-complement halves cancel modulo 2^32).
+// SOFT4 / FP32 (BMmax 16, D = 192: candidates within [-209, +723] units) fit with 4-stage fields, S = 5:
+// BASE = 8192, values in [1504, 31328).  (SOFT8's spread alone, D = 3072 units, leaves no room for a
+// history field in 16 bits; it stays on vd_decode_tg.)
 // So one v_add_u32 / v_sub_u32 adds for both chunks, v_pk_max_u16 takes both maxima, and the DPP exchange
 // rides on the subtraction (v_sub_u32_dpp: the partner's V minus the shared entry).  A DPP stage is
 // v_add_u32 + v_sub_u32_dpp + v_pk_max_u16 for two chunk-states, an LDS-exchange stage v_sub_u32 +
@@ -23,6 +26,11 @@
 // [guard | label-region table with the +tag area (TgTabLT<true>) | guard | ring A | ring B | guard]; two
 // rings in a wave's 5,120 B leave 6 slots each, so a traceback batch traces 5 words per chunk, both chunks'
 // words in one pass (lanes 0..4 chunk A, lanes 32..36 chunk B).
+//
+// Read-out.  J = 8 (HARD): SDWA shifts each half's field bits into byte g of its chunk's ring word.  J = 4
+// (SOFT4 / FP32): nibble g of the ring word; field pairs are gathered as c = (V >> 1) of the even field,
+// bfi(0x00F000F0, V << 3, c) of the odd one (chunk A's two fields in byte 0, chunk B's in byte 2), and at
+// the block end four v_perm_b32 turn the four pair words into the two ring words.
 #pragma once
 #include "vd_kernel_tg.h"
 
@@ -63,6 +71,15 @@ __device__ __forceinline__ void pk_stage_lds_post(uint32_t& V, uint32_t m, int p
         : "+{v60}"(V), "=&v"(a), "=&v"(b) : "v"(m), "v"(vp));
 }
 
+// metric format per input: history field length J, scale 2^S, base of a half
+template <int CH>
+struct PkFmt {
+    static constexpr int J = CH == HARD ? 8 : 4;
+    static constexpr int S = J + 1;
+    static constexpr uint32_t BASE = CH == HARD ? 16384u : 8192u;
+    static_assert(CH == HARD || CH == SOFT4 || CH == FP32, "int16 halves hold HARD, SOFT4 and FP32 metrics");
+};
+
 // LDS layout of a wave (words)
 struct PkLds {
     static constexpr int GW = kGuardWords;
@@ -75,13 +92,13 @@ struct PkLds {
 };
 static_assert(PkLds::TBS == 5 && kWaves * PkLds::WAVE * 4 <= 20480, "8 workgroups of 4 waves per CU");
 
-template <int CORE>
+template <int CH, int CORE>
 __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(8))) void vd_decode_pk(const void* __restrict__ in_all, void* __restrict__ out_all, Geom geo)
 {
-    using IN = TgIn<HARD>;
+    using IN = TgIn<CH>;
     using TT = TgTabLT<true>;
     using LL = PkLds;
-    constexpr int J = 8, S = 9;
+    constexpr int J = PkFmt<CH>::J, S = PkFmt<CH>::S;
     constexpr bool ALT = CORE == B32;  // M_B32: the upper position half takes the +tag entries at phase 0
     __shared__ __attribute__((aligned(16))) uint32_t lds[kWaves * LL::WAVE];
     const int lane = threadIdx.x & 63;
@@ -117,10 +134,11 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(8))
     // entry tag of the row's own class, both halves: tg0 * 65537 (M_FP16: own wins ties, +2^j; else -2^j)
     const int32_t tg0A = (CORE == F16 ? tagA : -tagA) * 65537, tg0B = (CORE == F16 ? tagB : -tagB) * 65537;
     const uint32_t tabl = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)tabb;
-    constexpr uint32_t BASE = 16384;
+    constexpr uint32_t BASE = PkFmt<CH>::BASE;
     constexpr uint32_t VB1 = BASE + (1u << (S - 1));  // a half with metric 0 and a cleared field
     constexpr uint32_t VBASE = VB1 * 65537u;
-    constexpr uint32_t FNM = 0xFE00FE00u, FHF = 0x01000100u;  // field clear: (V & FNM) | FHF, both halves
+    // field clear: (V & FNM) | FHF, both halves
+    constexpr uint32_t FNM = (0xFFFFu << S & 0xFFFFu) * 65537u, FHF = (1u << (S - 1)) * 65537u;
     Fair fair;
     fair.begin(batch + 1 < geo.nbatch ? nullptr : geo.fair, lane);
     const uint64_t availB = IN::bytes(geo.availStages);
@@ -130,9 +148,9 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(8))
     uint32_t V = VBASE;
     uint32_t kb = 0;
     uint32_t tbn = LL::TBS - (blockIdx.x & 3u);  // staggered first traceback batches
-    __amdgpu_buffer_rsrc_t rsA = tg_rsrc<HARD>(in, startA, availB), rsB = tg_rsrc<HARD>(in, startB, availB);
-    uint32_t rAA = IN::template load<0>(rsA, vo1), rBA = IN::template load<0>(rsA, vo2);
-    uint32_t rAB = IN::template load<0>(rsB, vo1), rBB = IN::template load<0>(rsB, vo2);
+    __amdgpu_buffer_rsrc_t rsA = tg_rsrc<CH>(in, startA, availB), rsB = tg_rsrc<CH>(in, startB, availB);
+    typename IN::raw_t rAA = IN::template load<0>(rsA, vo1), rBA = IN::template load<0>(rsA, vo2);
+    typename IN::raw_t rAB = IN::template load<0>(rsB, vo1), rBB = IN::template load<0>(rsB, vo2);
     // traceback roles: lanes 0..31 trace chunk A's words, 32..63 chunk B's
     const bool tbB = lane >= 32;
     const uint32_t tbl = (uint32_t)(lane & 31);
@@ -154,6 +172,8 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(8))
         constexpr int PH = decltype(PHc)::value;
         constexpr int BB = PH / 2;
         uint32_t wA = 0, wB = 0;
+        uint32_t cw[4];  // J = 4: field-pair words
+        (void)cw;
         sfor<32>([&](auto I) {
             constexpr int i = decltype(I)::value;
             constexpr int K = (PH + i) % 6;
@@ -168,30 +188,57 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(8))
             else pk_stage_lds_pre<true>(V, m, pa5);
             if constexpr (r + TGD < 96) issue(std::integral_constant<int, r + TGD>{});
             if constexpr (i % J == J - 1) {
-                // field read-out, both chunks: bits 1..8 of each half into byte g of its ring word (SDWA), then
-                // both fields cleared; at the block end the renormalisation on the whole word (vd_decode_tg)
+                // field read-out, both chunks, then both fields cleared; at the block end the renormalisation
+                // on the whole word (vd_decode_tg)
                 constexpr int g = (i % 32) / J;
                 uint32_t sr;
+#define VD_PK_RN "\n\ts_nop 0\n\tv_readfirstlane_b32 %[sr], %[V]\n\ts_sub_u32 %[sr], %[sr], %[vb]\n\tv_subrev_u32 %[V], %[sr], %[V]"
+#define VD_PK_IN [fnm] "v"(FNM), [fhf] "s"(FHF), [vb] "n"(VBASE)
+                if constexpr (J == 8) {
+                    // bits 1..8 of each half into byte g of its ring word (SDWA)
 #define VD_PK_RO(SEL, UNUSED)                                                                                \
     "v_lshrrev_b32_sdwa %[wa], 1, %[V] dst_sel:" SEL " dst_unused:" UNUSED " src0_sel:DWORD src1_sel:DWORD\n\t"  \
     "v_lshrrev_b32_sdwa %[wb], 1, %[V] dst_sel:" SEL " dst_unused:" UNUSED " src0_sel:DWORD src1_sel:WORD_1\n\t" \
     "v_and_or_b32 %[V], %[V], %[fnm], %[fhf]"
-#define VD_PK_RN "\n\ts_nop 0\n\tv_readfirstlane_b32 %[sr], %[V]\n\ts_sub_u32 %[sr], %[sr], %[vb]\n\tv_subrev_u32 %[V], %[sr], %[V]"
-#define VD_PK_IN [fnm] "v"(FNM), [fhf] "s"(FHF), [vb] "n"(VBASE)
-                if constexpr (g == 0)
-                    asm(VD_PK_RO("BYTE_0", "UNUSED_PAD") : [V] "+{v60}"(V), [wa] "=&v"(wA), [wb] "=&v"(wB) : VD_PK_IN);
-                else if constexpr (g == 1)
-                    asm(VD_PK_RO("BYTE_1", "UNUSED_PRESERVE") : [V] "+{v60}"(V), [wa] "+v"(wA), [wb] "+v"(wB) : VD_PK_IN);
-                else if constexpr (g == 2)
-                    asm(VD_PK_RO("BYTE_2", "UNUSED_PRESERVE") : [V] "+{v60}"(V), [wa] "+v"(wA), [wb] "+v"(wB) : VD_PK_IN);
-                else
-                    asm(VD_PK_RO("BYTE_3", "UNUSED_PRESERVE") VD_PK_RN
-                        : [V] "+{v60}"(V), [wa] "+v"(wA), [wb] "+v"(wB), [sr] "=&s"(sr) : VD_PK_IN : "scc");
+                    if constexpr (g == 0)
+                        asm(VD_PK_RO("BYTE_0", "UNUSED_PAD") : [V] "+{v60}"(V), [wa] "=&v"(wA), [wb] "=&v"(wB) : VD_PK_IN);
+                    else if constexpr (g == 1)
+                        asm(VD_PK_RO("BYTE_1", "UNUSED_PRESERVE") : [V] "+{v60}"(V), [wa] "+v"(wA), [wb] "+v"(wB) : VD_PK_IN);
+                    else if constexpr (g == 2)
+                        asm(VD_PK_RO("BYTE_2", "UNUSED_PRESERVE") : [V] "+{v60}"(V), [wa] "+v"(wA), [wb] "+v"(wB) : VD_PK_IN);
+                    else
+                        asm(VD_PK_RO("BYTE_3", "UNUSED_PRESERVE") VD_PK_RN
+                            : [V] "+{v60}"(V), [wa] "+v"(wA), [wb] "+v"(wB), [sr] "=&s"(sr) : VD_PK_IN : "scc");
+#undef VD_PK_RO
+                } else {
+                    // bits 1..4 of each half: the even field's as V >> 1, the odd field's (V << 3) into the
+                    // high nibbles of the pair word (chunk A byte 0, chunk B byte 2)
+                    constexpr uint32_t HN = 0x00F000F0u;
+#define VD_PK_RO4E "v_lshrrev_b32 %[c], 1, %[V]\n\tv_and_or_b32 %[V], %[V], %[fnm], %[fhf]"
+#define VD_PK_RO4O "v_lshlrev_b32 %[t], 3, %[V]\n\tv_and_or_b32 %[V], %[V], %[fnm], %[fhf]\n\tv_bfi_b32 %[c], %[hn], %[t], %[c]"
+                    uint32_t t;
+                    if constexpr (g % 2 == 0)
+                        asm(VD_PK_RO4E : [V] "+{v60}"(V), [c] "=&v"(cw[g / 2]) : VD_PK_IN);
+                    else if constexpr (g < 7)
+                        asm(VD_PK_RO4O : [V] "+{v60}"(V), [c] "+v"(cw[g / 2]), [t] "=&v"(t) : VD_PK_IN, [hn] "s"(HN));
+                    else
+                        asm(VD_PK_RO4O VD_PK_RN
+                            : [V] "+{v60}"(V), [c] "+v"(cw[g / 2]), [t] "=&v"(t), [sr] "=&s"(sr) : VD_PK_IN, [hn] "s"(HN)
+                            : "scc");
+#undef VD_PK_RO4E
+#undef VD_PK_RO4O
+                }
 #undef VD_PK_IN
 #undef VD_PK_RN
-#undef VD_PK_RO
             }
         });
+        if constexpr (J == 4) {
+            // pair words c0..c3 -> ring words: A = bytes 0 of c0..c3, B = bytes 2
+            const uint32_t p01 = __builtin_amdgcn_perm(cw[1], cw[0], 0x06020400u);
+            const uint32_t p23 = __builtin_amdgcn_perm(cw[3], cw[2], 0x06020400u);
+            wA = __builtin_amdgcn_perm(p23, p01, 0x05040100u);
+            wB = __builtin_amdgcn_perm(p23, p01, 0x07060302u);
+        }
         if constexpr (CORE == F16) {
             wA = ~wA;
             wB = ~wB;
@@ -206,7 +253,7 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(8))
             const uint32_t nw = j - 1 - kb;
             const uint32_t k = kb + tbl;
             if (tbl < nw && k < tbW) {
-                const TbC tc = tb_direct<J, CORE == B32>((int)k);
+                const TbC tc = tb_direct<(J < 6 ? 6 : J), CORE == B32>((int)k);
                 tbout[k] = traceback_word_tg<J, CORE == B32>(tbring, (tbl + 1u) * 256u, tc);
             }
             wave_sync();
@@ -218,8 +265,8 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(8))
         return j + 1 < nblk;
     };
     // the four entries of a stage for both chunks: E[L] = BM[L] * 2^S + tg0 per half (TgFmt::INT's table),
-    // from (A, B) = (BM[3], BM[2]) of each chunk packed as A_A + A_B * 2^16 (signed halves, |.| <= 1: an i24)
-    auto put_row = [&](auto PT, uint32_t wa, uint32_t wb, int li, int K) {
+    // from (A, B) = (BM[3], BM[2]) of each chunk packed as A_A + A_B * 2^16 (signed halves, |.| <= 16: an i24)
+    auto put_row = [&](auto PT, typename IN::raw_t wa, typename IN::raw_t wb, int li, int K) {
         constexpr int part = decltype(PT)::value;
         const int32_t tg = part ? tg0B : tg0A;
         int AA, BA, AB, BBv;
@@ -241,8 +288,8 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(8))
     for (uint32_t j = 0;; j += 3) {
         put_row(P0{}, rAA, rAB, sA, r6a);
         if (lane < 32) put_row(P1{}, rBA, rBB, sB, r6b);
-        rsA = tg_rsrc<HARD>(in, startA + 32ull * (j + 3), availB);
-        rsB = tg_rsrc<HARD>(in, startB + 32ull * (j + 3), availB);
+        rsA = tg_rsrc<CH>(in, startA + 32ull * (j + 3), availB);
+        rsB = tg_rsrc<CH>(in, startB + 32ull * (j + 3), availB);
         rAA = IN::template load<0>(rsA, vo1);
         rBA = IN::template load<0>(rsA, vo2);
         rAB = IN::template load<0>(rsB, vo1);

@@ -362,25 +362,41 @@ __device__ __forceinline__ uint32_t traceback_word_tg(const char* ringb, uint32_
         constexpr int BO = decltype(BOc)::value;  // 0: emit block, 2: convergence block
         constexpr int g = decltype(Gc)::value;
         constexpr int c = (BO + J * g + J - 1) % 6;
-        const uint32_t TX = T * ((1u << (J - 6)) | (1u << J));
-        const uint32_t p = __builtin_amdgcn_ubfe(TX, off[c / 2], 6u);
-        uint32_t W;
-        if constexpr (J == 8) W = *(const uint8_t*)(ringb + slot + 4 * p + g);
-        else W = *(const uint16_t*)(ringb + slot + 4 * p + 2 * g);
-        // the stride-6 suffix XOR of the field's J bits of W ^ T << (J-6) (bits >= J of Y: the copy of T)
-        uint32_t Y = W ^ TX;
-        if constexpr (J == 8) {
-            Y ^= __builtin_amdgcn_ubfe(Y, 6u, 2u);
+        if constexpr (J < 6) {
+            // 4-stage fields (vd_decode_pk's SOFT4 / FP32 kernels; nibble g of the ring word): every stage of
+            // the field touches a different position bit, so no suffix XOR; the field's decoded bits are
+            // W ^ (T >> (6 - J)) and the state at the field start keeps the low 6 - J bits of T (offsets:
+            // tb_direct<6, .>, TX = T | T << 6)
+            const uint32_t p = __builtin_amdgcn_ubfe(T * 65u, off[c / 2], 6u);
+            const uint32_t W = (uint32_t)(*(const uint8_t*)(ringb + slot + 4 * p + g / 2) >> (4 * (g % 2))) & JM;
+            uint32_t Y = W ^ (T >> (6 - J));
+            if constexpr (FIX5) {
+                constexpr int d = ((BO + J * g) % 6) / 2;
+                Y = (m5[d] & W) | (~m5[d] & Y);
+            }
+            T = ((T << J) | Y) & 63u;
+            return Y;
         } else {
-            Y ^= __builtin_amdgcn_ubfe(Y, 6u, 10u);
-            Y ^= __builtin_amdgcn_ubfe(Y, 12u, 4u);
+            const uint32_t TX = T * ((1u << (J - 6)) | (1u << J));
+            const uint32_t p = __builtin_amdgcn_ubfe(TX, off[c / 2], 6u);
+            uint32_t W;
+            if constexpr (J == 8) W = *(const uint8_t*)(ringb + slot + 4 * p + g);
+            else W = *(const uint16_t*)(ringb + slot + 4 * p + 2 * g);
+            // the stride-6 suffix XOR of the field's J bits of W ^ T << (J-6) (bits >= J of Y: the copy of T)
+            uint32_t Y = W ^ TX;
+            if constexpr (J == 8) {
+                Y ^= __builtin_amdgcn_ubfe(Y, 6u, 2u);
+            } else {
+                Y ^= __builtin_amdgcn_ubfe(Y, 6u, 10u);
+                Y ^= __builtin_amdgcn_ubfe(Y, 12u, 4u);
+            }
+            if constexpr (FIX5) {
+                constexpr int d = ((BO + J * g) % 6) / 2;
+                Y = (m5[d] & W) | (~m5[d] & Y);
+            }
+            T = Y & 63u;
+            return Y & JM;
         }
-        if constexpr (FIX5) {
-            constexpr int d = ((BO + J * g) % 6) / 2;
-            Y = (m5[d] & W) | (~m5[d] & Y);
-        }
-        T = Y & 63u;
-        return Y & JM;
     };
     sfor<G>([&](auto I) {  // convergence: block k+2, fields G-1 .. 0
         constexpr int g = G - 1 - decltype(I)::value;

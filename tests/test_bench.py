@@ -23,10 +23,10 @@ def test_algorithmic_bytes_match_survey():
 
 
 def test_mix_ceiling_from_committed_ablation():
-    for name in ("hard_b32", "soft8_b16"):
-        ms = bench.acs_only_ms(name)
-        assert ms is not None and 0.05 < ms < 0.5, (name, ms)
-    assert bench.acs_only_ms("fp32_f16") is None
+    ms = bench.acs_only_ms("soft8_b16")
+    assert ms is not None and 0.05 < ms < 0.5, ms
+    # the packed kernels (batched HARD, SOFT4, FP32) have no ablation, so no ceiling
+    assert bench.acs_only_ms("hard_b32") is None and bench.acs_only_ms("fp32_f16") is None
 
 
 def test_valu_view_from_committed_pmc():
@@ -38,11 +38,15 @@ def test_valu_view_from_committed_pmc():
         alg = bench.algorithmic_bytes(0x00 if name == "hard_b32" else 0x12, 2 * bench.N_BITS)
         assert alg <= p["traffic_bytes"] <= 1.2 * alg, (name, p["traffic_bytes"], alg)
         v = bench.valu_view(p, 0.18, 32_409_536, name, 31_999_936)
-        for k in ("insts_per_wave_stage", "issue_pct", "cycles_per_inst_per_simd", "pmc_run_clock_ghz",
-                  "issue_pct_live", "cycle_model_pct", "cycle_model_pct_live", "mix_ceiling"):
+        for k in ("insts_per_chunk_stage", "issue_pct", "cycles_per_inst_per_simd", "pmc_run_clock_ghz",
+                  "issue_pct_live", "cycle_model_pct", "cycle_model_pct_live"):
             assert k in v, (name, k)
+        # the fp32 tagged kernel has its ACS-only ceiling; the packed HARD kernel none
+        assert ("mix_ceiling" in v) == (name == "soft8_b16")
         assert "busy_pct" not in v  # the gfx94x SIMD-16 formula does not read as a percentage on gfx950
-        assert 3.0 < v["insts_per_wave_stage"] < 5.0
+        # per chunk-stage: ~3.9 VALU instructions on vd_decode_tg, ~2 on vd_decode_pk (two chunks per wave)
+        lo, hi = (3.0, 5.0) if name == "soft8_b16" else (1.2, 3.0)
+        assert lo < v["insts_per_chunk_stage"] < hi, v["insts_per_chunk_stage"]
         assert 1.5 < v["pmc_run_clock_ghz"] < 2.6
         # the cycle-weighted VALU model: the binding resource, well above the 2-cycle issue view
         assert v["issue_pct"] < v["cycle_model_pct"] <= 100.0

@@ -165,7 +165,9 @@ def group_traceback(words, J, core, t_end, n_groups):
         te = t0 + J - 1
         p = rotl6(T, te % 6)
         W = int(words[g][p])
-        Y = W ^ (T << (J - 6))
+        # J < 6 (vd_decode_pk's 4-stage fields): every stage of the field touches a different position bit,
+        # so no suffix XOR; the state at the field start keeps 6 - J bits of T
+        Y = W ^ (T << (J - 6)) if J >= 6 else W ^ (T >> (6 - J))
         o = Y
         sh = 6
         while sh < J:
@@ -177,7 +179,7 @@ def group_traceback(words, J, core, t_end, n_groups):
                     o = (o & ~(1 << jj)) | (W & (1 << jj))
         for jj in range(J):
             out_bits[t0 + jj] = (o >> jj) & 1
-        T = o & 63
+        T = o & 63 if J >= 6 else ((T << J) | o) & 63
     return out_bits
 
 
@@ -212,7 +214,10 @@ if __name__ == "__main__":
                               ("hard", "b16", 16, lambda: rng.integers(0, 2, 2)),
                               ("hard", "f16", 16, lambda: rng.integers(0, 2, 2)),
                               ("soft8", "b16", 8, lambda: rng.integers(-128, 128, 2)),
-                              ("soft8", "b32", 8, lambda: rng.integers(-128, 128, 2))]:
+                              ("soft8", "b32", 8, lambda: rng.integers(-128, 128, 2)),
+                              ("soft4", "b32", 4, lambda: rng.integers(-8, 8, 2)),
+                              ("soft4", "b16", 4, lambda: rng.integers(-8, 8, 2)),
+                              ("soft4", "f16", 4, lambda: rng.integers(-8, 8, 2))]:
         AB = []
         for _ in range(n):
             s = rngf()

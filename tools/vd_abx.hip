@@ -29,7 +29,7 @@ struct Variant { const char* name; KFn hard, soft8; int seg = vd::kSegPieces; ui
 #define VD_ABX_VARIANTS                                                                                      \
     {"fp32 tagged core (vd_decode_tg)", V<0>::hard, V<0>::soft8},                                           \
     {"batched hard: two chunks per wave (vd_decode_pk)", V<0>::hard, V<0>::soft8, vd::kSegPieces, vd::kSplitWarm, \
-     (KFn)vd::vd_decode_pk<vd::B32>},
+     (KFn)vd::vd_decode_pk<vd::HARD, vd::B32>},
 #endif
 
 static double median(std::vector<float> v)
