@@ -119,25 +119,28 @@ launch_fn pick_ob(int ob)
     return ob == 1 ? &launch_t<CH, CORE, 16> : &launch_t<CH, CORE, 32>;
 }
 
-// batched HARD / SOFT4 / FP32 launches with 32-bit output words: two chunks per wave in int16 halves
-// (vd_kernel_pk.h)
-template <int CH, int CORE>
+// batched HARD / SOFT4 / FP32 launches: two chunks per wave in int16 halves (vd_kernel_pk.h)
+template <int CH, int CORE, int OB>
 void launch_pk(const void* in, void* out, vd::Geom g, unsigned grid, hipStream_t s)
 {
-    hipLaunchKernelGGL((vd::vd_decode_pk<CH, CORE>), dim3(grid), dim3(64 * vd::kWaves), 0, s, in, out, g);
+    hipLaunchKernelGGL((vd::vd_decode_pk<CH, CORE, OB>), dim3(grid), dim3(64 * vd::kWaves), 0, s, in, out, g);
 }
-template <int CH>
+template <int CH, int OB>
 launch_fn pick_pk_core(int me)
 {
-    return me == 0 ? &launch_pk<CH, 0> : me == 1 ? &launch_pk<CH, 1> : &launch_pk<CH, 2>;
+    return me == 0 ? &launch_pk<CH, 0, OB> : me == 1 ? &launch_pk<CH, 1, OB> : &launch_pk<CH, 2, OB>;
+}
+template <int CH>
+launch_fn pick_pk_ob(int o)
+{
+    return out_of(o) == 1 ? pick_pk_core<CH, 16>(met_of(o)) : pick_pk_core<CH, 32>(met_of(o));
 }
 launch_fn pick_pk(int o)
 {
-    if (out_of(o) != 0) return nullptr;
     switch (ch_of(o)) {
-    case 0: return pick_pk_core<vd::HARD>(met_of(o));
-    case 1: return pick_pk_core<vd::SOFT4>(met_of(o));
-    case 4: return pick_pk_core<vd::FP32>(met_of(o));
+    case 0: return pick_pk_ob<vd::HARD>(o);
+    case 1: return pick_pk_ob<vd::SOFT4>(o);
+    case 4: return pick_pk_ob<vd::FP32>(o);
     }
     return nullptr;
 }

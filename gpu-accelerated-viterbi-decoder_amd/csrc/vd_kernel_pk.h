@@ -1,5 +1,5 @@
-// vd_kernel_pk.h -- vd_decode_pk<CH, CORE>: HARD, SOFT4 or FP32 input, TWO chunks per wave, one in each
-// 16-bit half of the lane's metric word (batched launches).  Same decode as vd_decode_tg<CH, CORE, 32> word
+// vd_kernel_pk.h -- vd_decode_pk<CH, CORE, OB>: HARD, SOFT4 or FP32 input, TWO chunks per wave, one in each
+// 16-bit half of the lane's metric word (batched launches).  Same decode as vd_decode_tg<CH, CORE, OB> word
 // for word (reference viterbi_core, src/viterbi/viterbi.cu:144-207; tie rules viterbiACS.cuh:113-157,216-256).
 //
 // Why it is exact.  A HARD metric needs few bits: every path metric lies within D = 12 units of the best
@@ -92,7 +92,7 @@ struct PkLds {
 };
 static_assert(PkLds::TBS == 5 && kWaves * PkLds::WAVE * 4 <= 20480, "8 workgroups of 4 waves per CU");
 
-template <int CH, int CORE>
+template <int CH, int CORE, int OB = 32>
 __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(8))) void vd_decode_pk(const void* __restrict__ in_all, void* __restrict__ out_all, Geom geo)
 {
     using IN = TgIn<CH>;
@@ -113,7 +113,7 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(8))
     const uint32_t batch = gc / geo.nchunks;
     const uint32_t cA = gc - batch * geo.nchunks;
     const void* const in = (const char*)in_all + batch * geo.inStride;
-    uint32_t* const out = (uint32_t*)((char*)out_all + batch * geo.outStride);
+    char* const out = (char*)out_all + batch * geo.outStride;
     const ChunkRange crA = chunk_range(geo, cA), crB = chunk_range(geo, cA + 1);
     if (crA.words == 0 && crB.words == 0) return;
     if (geo.check && lane < 3 * kGuardWords) wlds[LL::guard(lane)] = kGuardPattern;
@@ -143,8 +143,10 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(8))
     fair.begin(batch + 1 < geo.nbatch ? nullptr : geo.fair, lane);
     const uint64_t availB = IN::bytes(geo.availStages);
     const uint32_t vo1 = IN::voff(sA), vo2 = IN::voff(sB);
-    const uint32_t WA = crA.words, WB = crB.words, nblk = (WA > WB ? WA : WB) + 2;
-    const uint64_t startA = crA.startWord * 32ull, startB = crB.startWord * 32ull;
+    // 32-bit words traced per chunk (O_B16: each written as two 16-bit words, vd_decode_tg's policy)
+    const uint32_t WA = OB == 32 ? crA.words : (crA.words + 1) / 2, WB = OB == 32 ? crB.words : (crB.words + 1) / 2;
+    const uint32_t nblk = (WA > WB ? WA : WB) + 2;
+    const uint64_t startA = crA.startWord * (uint64_t)OB, startB = crB.startWord * (uint64_t)OB;
     uint32_t V = VBASE;
     uint32_t kb = 0;
     uint32_t tbn = LL::TBS - (blockIdx.x & 3u);  // staggered first traceback batches
@@ -155,7 +157,8 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(8))
     const bool tbB = lane >= 32;
     const uint32_t tbl = (uint32_t)(lane & 31);
     const char* const tbring = (const char*)(tbB ? ringB : ringA);
-    uint32_t* const tbout = out + (tbB ? crB.startWord : crA.startWord);
+    const uint64_t tbStart = tbB ? crB.startWord : crA.startWord;
+    const uint32_t tbWords = tbB ? crB.words : crA.words;
     const uint32_t tbW = tbB ? WB : WA;
 
     typedef uint32_t u2v __attribute__((ext_vector_type(2)));
@@ -254,7 +257,14 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(8))
             const uint32_t k = kb + tbl;
             if (tbl < nw && k < tbW) {
                 const TbC tc = tb_direct<(J < 6 ? 6 : J), CORE == B32>((int)k);
-                tbout[k] = traceback_word_tg<J, CORE == B32>(tbring, (tbl + 1u) * 256u, tc);
+                const uint32_t w = traceback_word_tg<J, CORE == B32>(tbring, (tbl + 1u) * 256u, tc);
+                if constexpr (OB == 32) {
+                    ((uint32_t*)out)[tbStart + k] = w;
+                } else {
+                    uint16_t* const o = (uint16_t*)out + tbStart;
+                    o[2 * k] = (uint16_t)(w >> 16);
+                    if (2 * k + 1 < tbWords) o[2 * k + 1] = (uint16_t)(w & 0xFFFFu);
+                }
             }
             wave_sync();
             ringA[pos] = wA;  // block j becomes slot 0 of the next batch

@@ -595,6 +595,11 @@ template <int CH>
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t tg_rsrc(const void* in, uint64_t g0, uint64_t availBytes)
 {
     const uint64_t off = TgIn<CH>::bytes(g0);
+    // the operands are wave-uniform; readfirstlane keeps them in SGPRs where the compiler's divergence
+    // analysis cannot see it (a no-op on values already scalar)
+    const uint32_t ol = __builtin_amdgcn_readfirstlane((uint32_t)off), oh = __builtin_amdgcn_readfirstlane((uint32_t)(off >> 32));
+    const uint32_t al = __builtin_amdgcn_readfirstlane((uint32_t)availBytes);
+    const uint32_t ah = __builtin_amdgcn_readfirstlane((uint32_t)(availBytes >> 32));
     uint32_t lo, hi;
     asm("s_sub_u32 %[lo], %[al], %[ol]\n\t"
         "s_subb_u32 %[hi], %[ah], %[oh]\n\t"  // SCC = borrow: the group starts past the data
@@ -603,10 +608,9 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t tg_rsrc(const void* in, uint64
         "s_cmp_lg_u32 %[hi], 0\n\t"
         "s_cselect_b32 %[lo], -1, %[lo]"
         : [lo] "=&s"(lo), [hi] "=&s"(hi)
-        : [al] "s"((uint32_t)availBytes), [ah] "s"((uint32_t)(availBytes >> 32)), [ol] "s"((uint32_t)off),
-          [oh] "s"((uint32_t)(off >> 32))
+        : [al] "s"(al), [ah] "s"(ah), [ol] "s"(ol), [oh] "s"(oh)
         : "scc");
-    return __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)in + off), (short)0, (int)lo, 0x00020000);
+    return __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)in + ((uint64_t)oh << 32 | ol)), (short)0, (int)lo, 0x00020000);
 }
 
 // ---------------------------------------------------------------- segment launches

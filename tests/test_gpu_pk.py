@@ -1,5 +1,6 @@
 """Batched HARD, SOFT4 and FP32 launches on vd_decode_pk (vd_kernel_pk.h): two chunks per wave, one in each
-16-bit half of the metric word (HARD: 8-stage history fields; SOFT4 / FP32: 4-stage fields).  Every batch must equal the oracle word for word and the fp32 tagged kernel's output
+16-bit half of the metric word (HARD: 8-stage history fields; SOFT4 / FP32: 4-stage fields), 32- and 16-bit
+output words.  Every batch must equal the oracle word for word and the fp32 tagged kernel's output
 (VD_NO_PK=1 at decoder creation selects it), for every metric core's tie rule, including chunk counts where
 the two chunks of a wave differ in length (an odd number of long chunks), partitions with empty chunks, and
 saturated inputs (SNR 15: the best path gains every stage, the largest range the int16 halves must hold)."""
@@ -9,7 +10,7 @@ import numpy as np
 import pytest
 import torch
 
-from vitdec import FP32, HARD, M_B16, M_B32, M_FP16, SOFT4
+from vitdec import FP32, HARD, M_B16, M_B32, M_FP16, O_B16, SOFT4
 from test_gpu_parity import name
 
 
@@ -45,7 +46,7 @@ def _decode_batched(gpu, opt, packed, stride, n, nb, no_pk):
     return out, ostride, nout
 
 
-PK_OPTS = [ch | me for ch in (HARD, SOFT4, FP32) for me in (M_B32, M_B16, M_FP16)]
+PK_OPTS = [ch | me for ch in (HARD, SOFT4, FP32) for me in (M_B32, M_B16, M_FP16)] + [HARD | M_B32 | O_B16, FP32 | M_FP16 | O_B16]
 
 
 def test_packed_kernel_names():
