@@ -120,27 +120,29 @@ launch_fn pick_ob(int ob)
 }
 
 // batched HARD / SOFT4 / FP32 launches: two chunks per wave in int16 halves (vd_kernel_pk.h)
-template <int CH, int CORE, int OB>
+// (SPL: single-batch launches, one chunk per wave in both halves, vd_kernel_pk.h "split")
+template <int CH, int CORE, int OB, bool SPL>
 void launch_pk(const void* in, void* out, vd::Geom g, unsigned grid, hipStream_t s)
 {
-    hipLaunchKernelGGL((vd::vd_decode_pk<CH, CORE, OB>), dim3(grid), dim3(64 * vd::kWaves), 0, s, in, out, g);
+    hipLaunchKernelGGL((vd::vd_decode_pk<CH, CORE, OB, SPL>), dim3(grid), dim3(64 * vd::kWaves), 0, s, in, out, g);
 }
-template <int CH, int OB>
+template <int CH, int OB, bool SPL>
 launch_fn pick_pk_core(int me)
 {
-    return me == 0 ? &launch_pk<CH, 0, OB> : me == 1 ? &launch_pk<CH, 1, OB> : &launch_pk<CH, 2, OB>;
+    return me == 0 ? &launch_pk<CH, 0, OB, SPL> : me == 1 ? &launch_pk<CH, 1, OB, SPL> : &launch_pk<CH, 2, OB, SPL>;
 }
-template <int CH>
+template <int CH, bool SPL>
 launch_fn pick_pk_ob(int o)
 {
-    return out_of(o) == 1 ? pick_pk_core<CH, 16>(met_of(o)) : pick_pk_core<CH, 32>(met_of(o));
+    return out_of(o) == 1 ? pick_pk_core<CH, 16, SPL>(met_of(o)) : pick_pk_core<CH, 32, SPL>(met_of(o));
 }
+template <bool SPL>
 launch_fn pick_pk(int o)
 {
     switch (ch_of(o)) {
-    case 0: return pick_pk_ob<vd::HARD>(o);
-    case 1: return pick_pk_ob<vd::SOFT4>(o);
-    case 4: return pick_pk_ob<vd::FP32>(o);
+    case 0: return pick_pk_ob<vd::HARD, SPL>(o);
+    case 1: return pick_pk_ob<vd::SOFT4, SPL>(o);
+    case 4: return pick_pk_ob<vd::FP32, SPL>(o);
     }
     return nullptr;
 }
@@ -169,26 +171,26 @@ launch_fn pick(int o, bool llr)
 const char* kname(int o)
 {
     static const char* names[5][3] = {
-        {"vd_decode_pk<HARD,B32> (batched: two chunks per lane in int16 halves) / vd_decode_tg<HARD,B32> (single batch: "
-         "fp32 tagged core); M_B32 tie rule",
-         "vd_decode_pk<HARD,B16> (batched: two chunks per lane in int16 halves) / vd_decode_tg<HARD,B16> (single batch: "
-         "fp32 tagged core); M_B16 tie rule",
-         "vd_decode_pk<HARD,F16> (batched: two chunks per lane in int16 halves) / vd_decode_tg<HARD,F16> (single batch: "
-         "fp32 tagged core); M_FP16 tie rule"},
-        {"vd_decode_pk<SOFT4,B32> (batched: two chunks per lane in int16 halves) / vd_decode_tg<SOFT4,B32> (single "
-         "batch: fp32 tagged core); M_B32 tie rule",
-         "vd_decode_pk<SOFT4,B16> (batched: two chunks per lane in int16 halves) / vd_decode_tg<SOFT4,B16> (single "
-         "batch: fp32 tagged core); M_B16 tie rule",
-         "vd_decode_pk<SOFT4,F16> (batched: two chunks per lane in int16 halves) / vd_decode_tg<SOFT4,F16> (single "
-         "batch: fp32 tagged core); M_FP16 tie rule"},
+        {"vd_decode_pk<HARD,B32> (int16 halves: batched, two chunks per lane; single batch, one chunk cut in two) / "
+         "vd_decode_tg<HARD,B32> (single batches with chunks under 64 words; fused LLR); M_B32 tie rule",
+         "vd_decode_pk<HARD,B16> (int16 halves: batched, two chunks per lane; single batch, one chunk cut in two) / "
+         "vd_decode_tg<HARD,B16> (single batches with chunks under 64 words; fused LLR); M_B16 tie rule",
+         "vd_decode_pk<HARD,F16> (int16 halves: batched, two chunks per lane; single batch, one chunk cut in two) / "
+         "vd_decode_tg<HARD,F16> (single batches with chunks under 64 words; fused LLR); M_FP16 tie rule"},
+        {"vd_decode_pk<SOFT4,B32> (int16 halves: batched, two chunks per lane; single batch, one chunk cut in two) / "
+         "vd_decode_tg<SOFT4,B32> (single batches with chunks under 64 words; fused LLR); M_B32 tie rule",
+         "vd_decode_pk<SOFT4,B16> (int16 halves: batched, two chunks per lane; single batch, one chunk cut in two) / "
+         "vd_decode_tg<SOFT4,B16> (single batches with chunks under 64 words; fused LLR); M_B16 tie rule",
+         "vd_decode_pk<SOFT4,F16> (int16 halves: batched, two chunks per lane; single batch, one chunk cut in two) / "
+         "vd_decode_tg<SOFT4,F16> (single batches with chunks under 64 words; fused LLR); M_FP16 tie rule"},
         {"vd_decode_tg<SOFT8,B32> (fp32 tagged core, M_B32 tie rule)", "vd_decode_tg<SOFT8,B16> (fp32 tagged core, M_B16 tie rule)", "-"},
         {"vd_decode_tg<SOFT16,B32> (int32 tagged patterns, M_B32 tie rule)", "-", "-"},
-        {"vd_decode_pk<FP32,B32> (batched: two chunks per lane in int16 halves) / vd_decode_tg<FP32,B32> (single "
-         "batch: fp32 tagged core); M_B32 tie rule",
-         "vd_decode_pk<FP32,B16> (batched: two chunks per lane in int16 halves) / vd_decode_tg<FP32,B16> (single "
-         "batch: fp32 tagged core); M_B16 tie rule",
-         "vd_decode_pk<FP32,F16> (batched: two chunks per lane in int16 halves) / vd_decode_tg<FP32,F16> (single "
-         "batch: fp32 tagged core); M_FP16 tie rule"},
+        {"vd_decode_pk<FP32,B32> (int16 halves: batched, two chunks per lane; single batch, one chunk cut in two) / "
+         "vd_decode_tg<FP32,B32> (single batches with chunks under 64 words; fused LLR); M_B32 tie rule",
+         "vd_decode_pk<FP32,B16> (int16 halves: batched, two chunks per lane; single batch, one chunk cut in two) / "
+         "vd_decode_tg<FP32,B16> (single batches with chunks under 64 words; fused LLR); M_B16 tie rule",
+         "vd_decode_pk<FP32,F16> (int16 halves: batched, two chunks per lane; single batch, one chunk cut in two) / "
+         "vd_decode_tg<FP32,F16> (single batches with chunks under 64 words; fused LLR); M_FP16 tie rule"},
     };
     if (!valid(o)) return "-";
     return names[ch_of(o)][met_of(o)];
@@ -226,8 +228,8 @@ struct vd_decoder {
     hipStream_t s_in = nullptr, s_out = nullptr;
     DeviceState* ds = nullptr;  // the device's board / segment tables (looked up once, vd_create)
     int split = 1;              // segment launches: 0 none (VD_NO_SPLIT=1), 1 pieces, 2 thirds, 3 sevenths (VD_SPLIT=...)
-    int pk = 1;                 // batched HARD/SOFT4/FP32 launches on vd_decode_pk (VD_NO_PK=1: on vd_decode_tg)
-    int pk1 = 0;                // single-batch launches on vd_decode_pk too (VD_PK_SINGLE=1; study)
+    int pk = 1;                 // HARD/SOFT4/FP32 launches on vd_decode_pk (VD_NO_PK=1: on vd_decode_tg)
+    int pksplit = 1;            // their single-batch launches split on vd_decode_pk (VD_PK_SPLIT=0: tg segments)
     uint32_t* check = nullptr;  // LDS guard violation counter (vd_set_guard_check), null = off
 };
 
@@ -341,9 +343,19 @@ static int launch_decode(const vd_decoder* d, const void* in_d, void* out_d, siz
     g.nbatch = nbatch;
     g.inStride = inStride;
     g.outStride = outStride;
-    launch_fn fp = (nbatch > 1 || d->pk1) && !llr && d->pk && g.nchunks % (2 * vd::kWaves) == 0 ? pick_pk(options) : nullptr;
+    launch_fn fp = nbatch > 1 && !llr && d->pk && g.nchunks % (2 * vd::kWaves) == 0 ? pick_pk<false>(options) : nullptr;
     if (fp) {  // two chunks per wave: nchunks * nbatch / 8 workgroups
         fp(in_d, out_d, g, (unsigned)((uint64_t)g.nchunks * nbatch / (2 * vd::kWaves)), s);
+        VD_HIP(hipGetLastError());
+        return VD_OK;
+    }
+    // single batch, chunks long enough to cut: one chunk per wave, cut in two halves (nchunks / 4 workgroups)
+    const uint64_t w32 = out_of(options) != 0 ? g.packNum / 2 : g.packNum;
+    fp = nbatch == 1 && !llr && d->pk && d->pksplit && d->split && g.nchunks % vd::kWaves == 0 &&
+                 w32 / g.nchunks >= (uint64_t)vd::kSplitMinWords ? pick_pk<true>(options) : nullptr;
+    if (fp) {
+        g.stats = d->ds->stats;
+        fp(in_d, out_d, g, g.nchunks / vd::kWaves, s);
         VD_HIP(hipGetLastError());
         return VD_OK;
     }
@@ -403,8 +415,8 @@ int vd_create(int options, size_t preallocInputNum, int device, vd_decoder** out
     d->split = nosplit && nosplit[0] == '1' ? 0 : smode && !strcmp(smode, "thirds") ? 2 : smode && !strcmp(smode, "sevenths") ? 3 : 1;
     const char* nopk = std::getenv("VD_NO_PK");
     d->pk = nopk && nopk[0] == '1' ? 0 : 1;
-    const char* pk1 = std::getenv("VD_PK_SINGLE");
-    d->pk1 = pk1 && pk1[0] == '1' ? 1 : 0;
+    const char* pks = std::getenv("VD_PK_SPLIT");
+    d->pksplit = pks && pks[0] == '0' ? 0 : 1;
     const char* chk = std::getenv("VD_CHECK");
     if (chk && chk[0] == '1') {
         int rc = vd_set_guard_check(d, 1);

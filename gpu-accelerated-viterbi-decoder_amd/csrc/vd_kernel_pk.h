@@ -92,8 +92,24 @@ struct PkLds {
 };
 static_assert(PkLds::TBS == 5 && kWaves * PkLds::WAVE * 4 <= 20480, "8 workgroups of 4 waves per CU");
 
-template <int CH, int CORE, int OB = 32>
-__global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(8))) void vd_decode_pk(const void* __restrict__ in_all, void* __restrict__ out_all, Geom geo)
+// Split single-batch launches (SPL): one chunk per wave, its first part in half A and its rest in half B.
+// Chunk c of W words is cut at word r (a multiple of 3 blocks, r ~ (W + 6) / 2): half A decodes blocks
+// 0 .. r+1 from the chunk start (equal metrics, as the chunk itself) and emits words 0 .. r-1; half B starts
+// kPkWarm blocks before block r from equal metrics and emits words r .. W-1.  Both origins are multiples of
+// 3 blocks apart, so both halves see the same stage phases in lockstep.  At the end of chunk block r-1
+// (A's block r-1, B's block kPkWarm-1) each half keeps its renormalised metric vector; equal vectors mean
+// equal decisions from block r on (the recursion and the tie rules depend on metric differences only), so
+// B's words are exact.  Otherwise a second pass re-decodes B's words from chunk block r with A's vector
+// (both halves then hold that chunk part; A writes nothing).  The result does not depend on timing.
+constexpr int kPkWarm = 6;
+__host__ __device__ constexpr uint32_t pk_split_word(uint32_t W)
+{
+    const uint32_t r = 3u * ((W + 6u + 3u) / 6u);  // 3 * round((W + 6) / 6)
+    return r < (uint32_t)kPkWarm ? (uint32_t)kPkWarm : r;
+}
+
+template <int CH, int CORE, int OB = 32, bool SPL = false>
+__global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(SPL ? 7 : 8))) void vd_decode_pk(const void* __restrict__ in_all, void* __restrict__ out_all, Geom geo)
 {
     using IN = TgIn<CH>;
     using TT = TgTabLT<true>;
@@ -108,13 +124,14 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(8))
     char* const tabb = (char*)(wlds + LL::TAB_OFF);
     uint32_t* const ringA = wlds + LL::RING_OFF;
     uint32_t* const ringB = ringA + LL::RING;
-    // chunks 2w, 2w+1 of the launch (batch b: launch chunks b * nchunks ..; nchunks is even)
-    const uint32_t gc = 2u * (blockIdx.x * kWaves + (uint32_t)wv);
-    const uint32_t batch = gc / geo.nchunks;
+    // batched: chunks 2w, 2w+1 of the launch (batch b: launch chunks b * nchunks ..; nchunks is even);
+    // SPL: chunk w, both halves
+    const uint32_t gc = SPL ? blockIdx.x * kWaves + (uint32_t)wv : 2u * (blockIdx.x * kWaves + (uint32_t)wv);
+    const uint32_t batch = SPL ? 0u : gc / geo.nchunks;
     const uint32_t cA = gc - batch * geo.nchunks;
     const void* const in = (const char*)in_all + batch * geo.inStride;
     char* const out = (char*)out_all + batch * geo.outStride;
-    const ChunkRange crA = chunk_range(geo, cA), crB = chunk_range(geo, cA + 1);
+    const ChunkRange crA = chunk_range(geo, cA), crB = SPL ? crA : chunk_range(geo, cA + 1);
     if (crA.words == 0 && crB.words == 0) return;
     if (geo.check && lane < 3 * kGuardWords) wlds[LL::guard(lane)] = kGuardPattern;
 
@@ -145,21 +162,32 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(8))
     const uint32_t vo1 = IN::voff(sA), vo2 = IN::voff(sB);
     // 32-bit words traced per chunk (O_B16: each written as two 16-bit words, vd_decode_tg's policy)
     const uint32_t WA = OB == 32 ? crA.words : (crA.words + 1) / 2, WB = OB == 32 ? crB.words : (crB.words + 1) / 2;
-    const uint32_t nblk = (WA > WB ? WA : WB) + 2;
-    const uint64_t startA = crA.startWord * (uint64_t)OB, startB = crB.startWord * (uint64_t)OB;
+    // the halves' jobs: first stage of the decode, and the local words k it emits, kmin <= k < kmax, as chunk
+    // words koff + k (local word k is traced from local blocks k + 1 and k + 2)
+    const uint32_t rs = SPL ? pk_split_word(WA) : 0u;  // SPL: the cut (chunk word / block index)
+    uint64_t startA = crA.startWord * (uint64_t)OB, startB = crB.startWord * (uint64_t)OB;
+    uint32_t kmaxA = WA, kminB = 0, kmaxB = WB, koffB = 0;
+    if constexpr (SPL) {
+        startB = startA + 32ull * (rs - kPkWarm);
+        kmaxA = rs;
+        kminB = kPkWarm;
+        kmaxB = WA - rs + kPkWarm;
+        koffB = rs - kPkWarm;
+    }
+    uint32_t nblk = (kmaxA > kmaxB ? kmaxA : kmaxB) + 2;
     uint32_t V = VBASE;
+    uint32_t snap = 0;  // SPL: B's metric half at the end of its warm-up (high), A's at chunk block rs-1 (low)
     uint32_t kb = 0;
     uint32_t tbn = LL::TBS - (blockIdx.x & 3u);  // staggered first traceback batches
     __amdgpu_buffer_rsrc_t rsA = tg_rsrc<CH>(in, startA, availB), rsB = tg_rsrc<CH>(in, startB, availB);
     typename IN::raw_t rAA = IN::template load<0>(rsA, vo1), rBA = IN::template load<0>(rsA, vo2);
     typename IN::raw_t rAB = IN::template load<0>(rsB, vo1), rBB = IN::template load<0>(rsB, vo2);
-    // traceback roles: lanes 0..31 trace chunk A's words, 32..63 chunk B's
+    // traceback roles: lanes 0..31 trace half A's words, 32..63 half B's
     const bool tbB = lane >= 32;
     const uint32_t tbl = (uint32_t)(lane & 31);
     const char* const tbring = (const char*)(tbB ? ringB : ringA);
     const uint64_t tbStart = tbB ? crB.startWord : crA.startWord;
     const uint32_t tbWords = tbB ? crB.words : crA.words;
-    const uint32_t tbW = tbB ? WB : WA;
 
     typedef uint32_t u2v __attribute__((ext_vector_type(2)));
     typedef __attribute__((address_space(3))) const volatile u2v* lptr;
@@ -246,6 +274,11 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(8))
             wA = ~wA;
             wB = ~wB;
         }
+        if constexpr (SPL) {
+            // block ends: B's warm-up end (block kPkWarm - 1) into the high half, A's block rs - 1 into the low
+            if (j == kPkWarm - 1) snap = V;
+            if (j == rs - 1) snap = __builtin_amdgcn_perm(snap, V, 0x07060100u);
+        }
         wave_sync();
         if (j >= 1) {
             ringA[(j - 1 - kb) * 64 + pos] = wA;
@@ -255,15 +288,16 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(8))
             wave_sync();
             const uint32_t nw = j - 1 - kb;
             const uint32_t k = kb + tbl;
-            if (tbl < nw && k < tbW) {
+            if (tbl < nw && k >= (tbB ? kminB : 0u) && k < (tbB ? kmaxB : kmaxA)) {
                 const TbC tc = tb_direct<(J < 6 ? 6 : J), CORE == B32>((int)k);
                 const uint32_t w = traceback_word_tg<J, CORE == B32>(tbring, (tbl + 1u) * 256u, tc);
+                const uint32_t kc = k + (tbB ? koffB : 0u);  // chunk word
                 if constexpr (OB == 32) {
-                    ((uint32_t*)out)[tbStart + k] = w;
+                    ((uint32_t*)out)[tbStart + kc] = w;
                 } else {
                     uint16_t* const o = (uint16_t*)out + tbStart;
-                    o[2 * k] = (uint16_t)(w >> 16);
-                    if (2 * k + 1 < tbWords) o[2 * k + 1] = (uint16_t)(w & 0xFFFFu);
+                    o[2 * kc] = (uint16_t)(w >> 16);
+                    if (2 * kc + 1 < tbWords) o[2 * kc + 1] = (uint16_t)(w & 0xFFFFu);
                 }
             }
             wave_sync();
@@ -295,22 +329,45 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(8))
     const int r6a = sA % 6, r6b = sB % 6;
     using P0 = std::integral_constant<int, 0>;
     using P1 = std::integral_constant<int, 1>;
-    for (uint32_t j = 0;; j += 3) {
-        put_row(P0{}, rAA, rAB, sA, r6a);
-        if (lane < 32) put_row(P1{}, rBA, rBB, sB, r6b);
-        rsA = tg_rsrc<CH>(in, startA + 32ull * (j + 3), availB);
-        rsB = tg_rsrc<CH>(in, startB + 32ull * (j + 3), availB);
+    for (int pass = 0;; pass++) {
+        for (uint32_t j = 0;; j += 3) {
+            put_row(P0{}, rAA, rAB, sA, r6a);
+            if (lane < 32) put_row(P1{}, rBA, rBB, sB, r6b);
+            rsA = tg_rsrc<CH>(in, startA + 32ull * (j + 3), availB);
+            rsB = tg_rsrc<CH>(in, startB + 32ull * (j + 3), availB);
+            rAA = IN::template load<0>(rsA, vo1);
+            rBA = IN::template load<0>(rsA, vo2);
+            rAB = IN::template load<0>(rsB, vo1);
+            rBB = IN::template load<0>(rsB, vo2);
+            if ((j / 3) % 2 == 0) fair.group(j, 3u, lane);
+            wave_sync();
+            sfor<TGD>([&](auto X) { issue(X); });
+            if (!block(std::integral_constant<int, 0>{}, j)) break;
+            if (!block(std::integral_constant<int, 2>{}, j + 1)) break;
+            if (!block(std::integral_constant<int, 4>{}, j + 2)) break;
+            wave_sync();
+        }
+        if constexpr (!SPL) break;
+        // SPL: B's words are exact when its vector equals A's at chunk block rs - 1 in every lane
+        if (pass == 1 || __builtin_amdgcn_ballot_w64((snap & 0xFFFFu) != (snap >> 16)) == 0) break;
+        if (lane == 0 && geo.stats) atomicAdd(geo.stats, 1u);  // counted like a segment re-decode
+        // re-decode B's words rs .. W-1 from chunk block rs with A's vector, in both halves (A writes nothing)
+        V = (snap & 0xFFFFu) * 65537u;
+        startA = startB = crA.startWord * (uint64_t)OB + 32ull * rs;
+        kmaxA = 0;
+        kminB = 0;
+        kmaxB = WA - rs;
+        koffB = rs;
+        nblk = kmaxB + 2;
+        kb = 0;
+        tbn = LL::TBS - (blockIdx.x & 3u);
+        wave_sync();
+        rsA = tg_rsrc<CH>(in, startA, availB);
+        rsB = rsA;
         rAA = IN::template load<0>(rsA, vo1);
         rBA = IN::template load<0>(rsA, vo2);
-        rAB = IN::template load<0>(rsB, vo1);
-        rBB = IN::template load<0>(rsB, vo2);
-        if ((j / 3) % 2 == 0) fair.group(j, 3u, lane);
-        wave_sync();
-        sfor<TGD>([&](auto X) { issue(X); });
-        if (!block(std::integral_constant<int, 0>{}, j)) break;
-        if (!block(std::integral_constant<int, 2>{}, j + 1)) break;
-        if (!block(std::integral_constant<int, 4>{}, j + 2)) break;
-        wave_sync();
+        rAB = rAA;
+        rBB = rBA;
     }
     fair.end(lane);
     if (geo.check) {

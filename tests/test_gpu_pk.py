@@ -71,3 +71,68 @@ def test_packed_batches_equal_oracle_and_fp32_kernel(gpu, vo, opt, nbits, snr):
         bad = np.flatnonzero(got != ref)
         assert bad.size == 0, f"batch {b}: {bad.size} of {ref.size} words differ (pack {pack}, rem {pack % 6400}), first {bad[:5]}"
         assert torch.equal(pk[b * ostride:b * ostride + nout], tg[b * ostride:b * ostride + nout])
+
+
+def _single(gpu, opt, packed_t, nin, n, env):
+    import vitdec  # noqa: F401
+    nout = gpu.lib().vd_output_size(opt, n)
+    out = torch.full((nout + 256,), 0x5A, dtype=torch.uint8, device="cuda")
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
+    try:
+        with gpu.ViterbiCUDA(opt) as dec:
+            dec.run_device(packed_t.data_ptr(), out.data_ptr(), n)
+            torch.cuda.synchronize()
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    assert bool((out[nout:] == 0x5A).all())  # nothing written past the output
+    return out[:nout]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("opt", [HARD | M_B32, HARD | M_B16, HARD | M_FP16, SOFT4 | M_B32, FP32 | M_FP16,
+                                 HARD | M_B32 | O_B16, FP32 | M_FP16 | O_B16], ids=name)
+@pytest.mark.parametrize("nbits,snr", [(13_107_264, 1.0), (20_000_000, 0.0), (9_000_000, 2.0), (32_000_000, 15.0)])
+def test_packed_split_single_launch(gpu, vo, opt, nbits, snr):
+    """Single-batch launches on vd_decode_pk's split kernel (one chunk per wave, cut at a multiple of 3 blocks,
+    the second part started 6 blocks early and checked at the cut): equal to vd_decode_tg's segment launch
+    (VD_PK_SPLIT=0), to the unsplit launch (VD_NO_SPLIT=1) and to the oracle.  13.1M bits: 64 words per chunk
+    (the smallest split); 9M bits: below it (not split)."""
+    n = 2 * nbits
+    packed, stride, nin = _batches(gpu, opt, nbits, snr, 1, 91)
+    before = gpu.split_redecodes()
+    pk = _single(gpu, opt, packed, nin, n, {})
+    redec = gpu.split_redecodes() - before
+    tg = _single(gpu, opt, packed, nin, n, {"VD_PK_SPLIT": "0"})
+    whole = _single(gpu, opt, packed, nin, n, {"VD_NO_SPLIT": "1"})
+    p = packed[:nin].cpu().numpy().view(np.int32)
+    ref, ok = vo.decode(opt, p, input_num=n, nthreads=16)
+    got = pk.cpu().numpy().view(ref.dtype)
+    bad = np.flatnonzero(got != ref)
+    assert bad.size == 0, f"{bad.size} of {ref.size} words differ (re-decoded: {redec}), first {bad[:5]}"
+    assert torch.equal(pk, tg) and torch.equal(pk, whole)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("opt", [HARD | M_B32, SOFT4 | M_B16], ids=name)
+def test_packed_split_random_input_redecodes(gpu, vo, opt):
+    """Uniformly random channel words: the second part's speculative start does not converge, so (nearly)
+    every chunk takes the re-decode pass, and the words still equal the oracle's."""
+    nbits = 16_000_000
+    n = 2 * nbits
+    nin = gpu.lib().vd_input_size(opt, n)
+    g = torch.Generator(device="cpu").manual_seed(5)
+    packed = torch.randint(0, 256, (nin + 256,), dtype=torch.uint8, generator=g).to("cuda")
+    before = gpu.split_redecodes()
+    pk = _single(gpu, opt, packed, nin, n, {})
+    redec = gpu.split_redecodes() - before
+    p = packed[:nin].cpu().numpy().view(np.int32)
+    ref, ok = vo.decode(opt, p, input_num=n, nthreads=16)
+    got = pk.cpu().numpy().view(ref.dtype)
+    bad = np.flatnonzero(got != ref)
+    assert bad.size == 0, f"{bad.size} of {ref.size} words differ (re-decoded: {redec}), first {bad[:5]}"
+    assert redec > 3000, redec

@@ -4,7 +4,10 @@ chunks in 4 segments that cross chunk boundaries).  A segment that starts inside
 speculatively and is checked at its boundary after a workgroup barrier; one whose check fails
 re-decodes from its left neighbour's end vector.  The decoded words must be identical to the unsplit launch (VD_NO_SPLIT=1) and
 to the oracle, at SNRs where the speculation always converges and where it often does not (SNR 0: the
-re-decode passes run, and the test requires that they did)."""
+re-decode passes run, and the test requires that they did).  HARD, SOFT4 and FP32 single launches run
+vd_decode_pk's split launch by default (mode "pk": one chunk per wave, its second part in the other int16
+half with a speculative start, checked at the cut, re-decoded from the first part's vector when it
+differs); "pieces" / "thirds" set VD_PK_SPLIT=0 to test vd_decode_tg's segment tables on them too."""
 import os
 
 import numpy as np
@@ -14,14 +17,29 @@ from vitdec import FP32, HARD, M_B16, M_B32, M_FP16, O_B16, SOFT4, SOFT8, SOFT16
 from test_gpu_parity import gpu_decode, name
 
 
+PK_CH = (HARD, SOFT4, FP32)
+
+
+def set_mode(mode):
+    """environment of a decoder created next: 'pk' = the default (vd_decode_pk split for HARD/SOFT4/FP32),
+    'pieces' / 'thirds' = vd_decode_tg segment tables for every format"""
+    if mode in ("pieces", "thirds"):
+        os.environ["VD_SPLIT"] = mode
+        os.environ["VD_PK_SPLIT"] = "0"
+
+
+def clear_mode():
+    os.environ.pop("VD_SPLIT", None)
+    os.environ.pop("VD_PK_SPLIT", None)
+
+
 def decode_split_and_whole(gpu, opt, packed, n, mode=None):
     before = gpu.split_redecodes()
-    if mode:
-        os.environ["VD_SPLIT"] = mode
+    set_mode(mode)
     try:
         out = gpu_decode(gpu, opt, packed)
     finally:
-        os.environ.pop("VD_SPLIT", None)
+        clear_mode()
     redecodes = gpu.split_redecodes() - before
     os.environ["VD_NO_SPLIT"] = "1"
     try:
@@ -35,8 +53,10 @@ def decode_split_and_whole(gpu, opt, packed, n, mode=None):
 @pytest.mark.parametrize("opt", [HARD | M_B32, SOFT8 | M_B16, SOFT4 | M_B32, FP32 | M_FP16, SOFT16 | M_B32,
                                  HARD | M_B32 | O_B16, SOFT8 | M_B16 | O_B16, FP32 | M_FP16 | O_B16], ids=name)
 @pytest.mark.parametrize("snr", [0.0, 1.0, 3.0])
-@pytest.mark.parametrize("mode", ["pieces", "thirds"])
+@pytest.mark.parametrize("mode", ["pieces", "thirds", "pk"])
 def test_split_equals_whole_16m(gpu, vo, opt, snr, mode):
+    if mode == "pk" and (opt & 0xF) not in PK_CH:
+        pytest.skip("no packed kernel for this input format")
     # 78 32-bit words per chunk: segment launch (>= 64); O_B16: 156-157 16-bit words per chunk (odd
     # counts: the last segment of a chunk writes its final half word only).  pieces: 256 chunks in 4
     # pieces; thirds: workgroups of 3 (4) chunks in 4 segments, segments crossing chunk boundaries
@@ -68,15 +88,17 @@ def gpu_sim(gpu, opt, n, snr):
 @pytest.mark.slow
 @pytest.mark.parametrize("snr", [0.0, 1.2])
 @pytest.mark.parametrize("opt", [HARD | M_B32, SOFT8 | M_B16], ids=name)
-@pytest.mark.parametrize("mode", ["pieces", "thirds"])
+@pytest.mark.parametrize("mode", ["pieces", "thirds", "pk"])
 def test_split_full_32m_matches_oracle(gpu, vo, opt, snr, mode):
+    if mode == "pk" and (opt & 0xF) not in PK_CH:
+        pytest.skip("no packed kernel for this input format")
     bits, packed = gpu_sim(gpu, opt, 32_000_000, snr)
     before = gpu.split_redecodes()
-    os.environ["VD_SPLIT"] = mode
+    set_mode(mode)
     try:
         out = gpu_decode(gpu, opt, packed)
     finally:
-        os.environ.pop("VD_SPLIT", None)
+        clear_mode()
     redecodes = gpu.split_redecodes() - before
     ref, ok = vo.decode(opt, packed, nthreads=16)
     assert ok
