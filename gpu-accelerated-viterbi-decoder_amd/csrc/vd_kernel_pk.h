@@ -80,17 +80,19 @@ struct PkFmt {
     static_assert(CH == HARD || CH == SOFT4 || CH == FP32, "int16 halves hold HARD, SOFT4 and FP32 metrics");
 };
 
-// LDS layout of a wave (words)
+// LDS layout of a wave (words), for NW resident workgroups (waves per SIMD) per CU
+template <int NW = 8>
 struct PkLds {
     static constexpr int GW = kGuardWords;
     static constexpr int TAB = TgTabLT<true>::BYTES / 4;
-    static constexpr int TBS = (kWaveLdsWords - 3 * GW - TAB) / 128 - 1;  // words per traceback batch and chunk
+    static constexpr int LDSW = 163840 / 4 / (NW * kWaves);                // a wave's share
+    static constexpr int TBS = (LDSW - 3 * GW - TAB) / 128 - 1;            // words per traceback batch and chunk
     static constexpr int RING = (TBS + 1) * 64;                            // words per chunk ring
     static constexpr int TAB_OFF = GW, RING_OFF = 2 * GW + TAB;
     static constexpr int WAVE = 3 * GW + TAB + 2 * RING;
     static __device__ __forceinline__ int guard(int i) { return i < GW ? i : i < 2 * GW ? TAB + i : TAB + 2 * RING + i; }
 };
-static_assert(PkLds::TBS == 5 && kWaves * PkLds::WAVE * 4 <= 20480, "8 workgroups of 4 waves per CU");
+static_assert(PkLds<8>::TBS == 5 && kWaves * PkLds<8>::WAVE * 4 <= 20480, "8 workgroups of 4 waves per CU");
 
 // Split single-batch launches (SPL): one chunk per wave, its first part in half A and its rest in half B.
 // Chunk c of W words is cut at word r (a multiple of 3 blocks, r ~ (W + 6) / 2): half A decodes blocks
@@ -108,12 +110,12 @@ __host__ __device__ constexpr uint32_t pk_split_word(uint32_t W)
     return r < (uint32_t)kPkWarm ? (uint32_t)kPkWarm : r;
 }
 
-template <int CH, int CORE, int OB = 32, bool SPL = false>
-__global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(SPL ? 7 : 8))) void vd_decode_pk(const void* __restrict__ in_all, void* __restrict__ out_all, Geom geo)
+template <int CH, int CORE, int OB = 32, bool SPL = false, int NW = 8>
+__global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(SPL ? 7 : NW))) void vd_decode_pk(const void* __restrict__ in_all, void* __restrict__ out_all, Geom geo)
 {
     using IN = TgIn<CH>;
     using TT = TgTabLT<true>;
-    using LL = PkLds;
+    using LL = PkLds<NW>;
     constexpr int J = PkFmt<CH>::J, S = PkFmt<CH>::S;
     constexpr bool ALT = CORE == B32;  // M_B32: the upper position half takes the +tag entries at phase 0
     __shared__ __attribute__((aligned(16))) uint32_t lds[kWaves * LL::WAVE];

@@ -27,9 +27,12 @@ struct V {
 struct Variant { const char* name; KFn hard, soft8; int seg = vd::kSegPieces; uint32_t warm = vd::kSplitWarm; KFn hardBatched = nullptr; };
 #ifndef VD_ABX_VARIANTS
 #define VD_ABX_VARIANTS                                                                                      \
-    {"fp32 tagged core (vd_decode_tg)", V<0>::hard, V<0>::soft8},                                           \
-    {"batched hard: two chunks per wave (vd_decode_pk)", V<0>::hard, V<0>::soft8, vd::kSegPieces, vd::kSplitWarm, \
-     (KFn)vd::vd_decode_pk<vd::HARD, vd::B32>},
+    {"vd_decode_pk, 8 waves/SIMD (TBS 5)", V<0>::hard, V<0>::soft8, vd::kSegPieces, vd::kSplitWarm,          \
+     (KFn)vd::vd_decode_pk<vd::HARD, vd::B32>},                                                             \
+    {"vd_decode_pk, 7 waves/SIMD (TBS 6)", V<0>::hard, V<0>::soft8, vd::kSegPieces, vd::kSplitWarm,          \
+     (KFn)vd::vd_decode_pk<vd::HARD, vd::B32, 32, false, 7>},                                               \
+    {"vd_decode_pk, 6 waves/SIMD (TBS 8)", V<0>::hard, V<0>::soft8, vd::kSegPieces, vd::kSplitWarm,          \
+     (KFn)vd::vd_decode_pk<vd::HARD, vd::B32, 32, false, 6>},
 #endif
 
 static double median(std::vector<float> v)
