@@ -153,10 +153,10 @@ int vd_mt_state_after(uint32_t seed, uint64_t n, uint32_t* state624);
 long long vd_count_errors(int options, const uint8_t* bits, size_t N, const void* decoded, size_t decodedBytes);
 
 /* ---- runtime info ---- */
-/* split launches (DESIGN.md §4 "load balance"): how many pieces of split chunks were re-decoded on a
- * device because their speculative start had not converged at the piece boundary (all launches so far;
- * decoded words are exact either way).  VD_NO_SPLIT=1 in the environment (read once per process and
- * device) disables splitting. */
+/* split launches (DESIGN.md §4 "load balance"): how many pieces of split chunks (vd_decode_tg segment
+ * launches) or second chunk parts (vd_decode_pk split launches) were re-decoded on a device because their
+ * speculative start had not converged at the boundary (all launches so far; decoded words are exact either
+ * way).  VD_NO_SPLIT=1 in the environment (read at vd_create) disables splitting. */
 int vd_split_redecodes(int device, uint64_t* count);
 /* LDS guard check (tests): enable != 0 makes every later launch of this decoder write guard words around
  * each wave's branch-metric table and survivor ring in LDS and count, at kernel exit, the guard words
