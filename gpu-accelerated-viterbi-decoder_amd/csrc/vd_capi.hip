@@ -230,6 +230,7 @@ struct vd_decoder {
     int split = 1;              // segment launches: 0 none (VD_NO_SPLIT=1), 1 pieces, 2 thirds, 3 sevenths (VD_SPLIT=...)
     int pk = 1;                 // HARD/SOFT4/FP32 launches on vd_decode_pk (VD_NO_PK=1: on vd_decode_tg)
     int pksplit = 1;            // their single-batch launches split on vd_decode_pk (VD_PK_SPLIT=0: tg segments)
+    int pktail = 1;             // ... with the tail chunks in 4-wave workgroups (VD_PK_TAIL=0: one chunk per wave)
     uint32_t* check = nullptr;  // LDS guard violation counter (vd_set_guard_check), null = off
 };
 
@@ -355,7 +356,15 @@ static int launch_decode(const vd_decoder* d, const void* in_d, void* out_d, siz
                  w32 / g.nchunks >= (uint64_t)vd::kSplitMinWords ? pick_pk<true>(options) : nullptr;
     if (fp) {
         g.stats = d->ds->stats;
-        fp(in_d, out_d, g, g.nchunks / vd::kWaves, s);
+        // the last nchunks mod (SIMDs) chunks one per workgroup of 4 waves (8 parts each): with 6400 chunks
+        // on 1024 SIMDs every SIMD then runs 6 whole-chunk waves and one short one (vd_kernel_pk.h "split")
+        const uint32_t per = (uint32_t)d->ds->nsimd, tailc = per ? g.nchunks % per : 0u;
+        unsigned grid = g.nchunks / vd::kWaves;
+        if (d->pktail && tailc) {
+            g.tailWG = (g.nchunks - tailc) / vd::kWaves;
+            grid = g.tailWG + tailc;
+        }
+        fp(in_d, out_d, g, grid, s);
         VD_HIP(hipGetLastError());
         return VD_OK;
     }
@@ -417,6 +426,8 @@ int vd_create(int options, size_t preallocInputNum, int device, vd_decoder** out
     d->pk = nopk && nopk[0] == '1' ? 0 : 1;
     const char* pks = std::getenv("VD_PK_SPLIT");
     d->pksplit = pks && pks[0] == '0' ? 0 : 1;
+    const char* pkt = std::getenv("VD_PK_TAIL");
+    d->pktail = pkt && pkt[0] == '0' ? 0 : 1;
     const char* chk = std::getenv("VD_CHECK");
     if (chk && chk[0] == '1') {
         int rc = vd_set_guard_check(d, 1);

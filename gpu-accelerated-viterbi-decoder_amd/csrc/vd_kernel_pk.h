@@ -94,20 +94,26 @@ struct PkLds {
 };
 static_assert(PkLds<8>::TBS == 5 && kWaves * PkLds<8>::WAVE * 4 <= 20480, "8 workgroups of 4 waves per CU");
 
-// Split single-batch launches (SPL): one chunk per wave, its first part in half A and its rest in half B.
-// Chunk c of W words is cut at word r (a multiple of 3 blocks, r ~ (W + 6) / 2): half A decodes blocks
-// 0 .. r+1 from the chunk start (equal metrics, as the chunk itself) and emits words 0 .. r-1; half B starts
-// kPkWarm blocks before block r from equal metrics and emits words r .. W-1.  Both origins are multiples of
-// 3 blocks apart, so both halves see the same stage phases in lockstep.  At the end of chunk block r-1
-// (A's block r-1, B's block kPkWarm-1) each half keeps its renormalised metric vector; equal vectors mean
-// equal decisions from block r on (the recursion and the tie rules depend on metric differences only), so
-// B's words are exact.  Otherwise a second pass re-decodes B's words from chunk block r with A's vector
-// (both halves then hold that chunk part; A writes nothing).  The result does not depend on timing.
+// Split single-batch launches (SPL).  A chunk of W words is cut into P parts at words cut(1) .. cut(P-1),
+// multiples of 3 blocks; part p emits words [cut(p), cut(p+1)).  Part 0 decodes from the chunk start (equal
+// metrics, as the chunk itself); part p >= 1 starts kPkWarm blocks before block cut(p) from equal metrics.
+// Every origin is a multiple of 3 blocks, so the two halves of a wave see the same stage phases, table
+// rows and tags in lockstep.  A wave decodes parts 2q (half A) and 2q+1 (half B).  Part p's metric vector
+// at the end of chunk block cut(p)-1 (its start vector) and part p-1's at the same block (its end vector)
+// are kept (renormalised; one VGPR holds two halves); equal vectors mean equal decisions from block cut(p)
+// on (the recursion and the tie rules depend on metric differences only), so part p's words are exact.
+// After each pass every part whose start vector differs from its left neighbour's end vector is decoded
+// again from block cut(p) with that end vector; after pass k parts 0 .. k are exact, so the passes end
+// (at most P; the result never depends on timing).
+//  * Most chunks: one chunk per wave, P = 2 (the check is within the wave).
+//  * The last nchunks mod 4 NCU chunks (tail workgroups, Geom::tailWG): one chunk per workgroup of 4 waves,
+//    P = 8, so every SIMD gets 6 whole-chunk waves and one short one instead of 7 whole-chunk waves on a
+//    quarter of the SIMDs; the end vectors cross waves through LDS after a workgroup barrier.
 constexpr int kPkWarm = 6;
-__host__ __device__ constexpr uint32_t pk_split_word(uint32_t W)
+__host__ __device__ constexpr uint32_t pk_cut(uint32_t p, uint32_t P, uint32_t W)
 {
-    const uint32_t r = 3u * ((W + 6u + 3u) / 6u);  // 3 * round((W + 6) / 6)
-    return r < (uint32_t)kPkWarm ? (uint32_t)kPkWarm : r;
+    // 6 + 3 * round(p (W - 6) / (3 P)) for 0 < p < P
+    return p == 0 ? 0u : p >= P ? W : 6u + 3u * ((2u * p * (W - 6u) + 3u * P) / (6u * P));
 }
 
 template <int CH, int CORE, int OB = 32, bool SPL = false, int NW = 8>
@@ -127,8 +133,10 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(SPL
     uint32_t* const ringA = wlds + LL::RING_OFF;
     uint32_t* const ringB = ringA + LL::RING;
     // batched: chunks 2w, 2w+1 of the launch (batch b: launch chunks b * nchunks ..; nchunks is even);
-    // SPL: chunk w, both halves
-    const uint32_t gc = SPL ? blockIdx.x * kWaves + (uint32_t)wv : 2u * (blockIdx.x * kWaves + (uint32_t)wv);
+    // SPL: chunk w, both halves; tail workgroups: one chunk, wave q its parts 2q, 2q+1
+    const bool tail = SPL && blockIdx.x >= geo.tailWG;
+    const uint32_t gc = !SPL ? 2u * (blockIdx.x * kWaves + (uint32_t)wv)
+                             : tail ? geo.tailWG * kWaves + (blockIdx.x - geo.tailWG) : blockIdx.x * kWaves + (uint32_t)wv;
     const uint32_t batch = SPL ? 0u : gc / geo.nchunks;
     const uint32_t cA = gc - batch * geo.nchunks;
     const void* const in = (const char*)in_all + batch * geo.inStride;
@@ -164,21 +172,31 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(SPL
     const uint32_t vo1 = IN::voff(sA), vo2 = IN::voff(sB);
     // 32-bit words traced per chunk (O_B16: each written as two 16-bit words, vd_decode_tg's policy)
     const uint32_t WA = OB == 32 ? crA.words : (crA.words + 1) / 2, WB = OB == 32 ? crB.words : (crB.words + 1) / 2;
-    // the halves' jobs: first stage of the decode, and the local words k it emits, kmin <= k < kmax, as chunk
-    // words koff + k (local word k is traced from local blocks k + 1 and k + 2)
-    const uint32_t rs = SPL ? pk_split_word(WA) : 0u;  // SPL: the cut (chunk word / block index)
-    uint64_t startA = crA.startWord * (uint64_t)OB, startB = crB.startWord * (uint64_t)OB;
-    uint32_t kmaxA = WA, kminB = 0, kmaxB = WB, koffB = 0;
+    // the halves' jobs: origin = first chunk block of the decode, and the local words k it emits,
+    // kmin <= k < kmax, as chunk words origin + k (local word k is traced from local blocks k + 1 and k + 2);
+    // SPL: the local blocks whose end vectors are kept (start ss, end se; ~0u: none)
+    const uint64_t stA = crA.startWord * (uint64_t)OB, stB = crB.startWord * (uint64_t)OB;
+    const uint32_t P = tail ? 2u * kWaves : 2u, pA = tail ? 2u * (uint32_t)wv : 0u, pB = pA + 1u;
+    uint32_t oA = 0, oB = 0, kminA = 0, kmaxA = WA, kminB = 0, kmaxB = WB;
+    uint32_t ssA = ~0u, seA = ~0u, ssB = ~0u, seB = ~0u;
     if constexpr (SPL) {
-        startB = startA + 32ull * (rs - kPkWarm);
-        kmaxA = rs;
+        const uint32_t cA0 = pk_cut(pA, P, WA), cA1 = pk_cut(pA + 1u, P, WA), cB1 = pk_cut(pB + 1u, P, WA);
+        oA = pA ? cA0 - kPkWarm : 0u;
+        kminA = pA ? kPkWarm : 0u;
+        kmaxA = cA1 - oA;
+        ssA = pA ? kminA - 1u : ~0u;
+        seA = kmaxA - 1u;
+        oB = cA1 - kPkWarm;
         kminB = kPkWarm;
-        kmaxB = WA - rs + kPkWarm;
-        koffB = rs - kPkWarm;
+        kmaxB = cB1 - oB;
+        ssB = kminB - 1u;
+        seB = pB + 1u < P ? kmaxB - 1u : ~0u;
     }
+    uint64_t startA = stA + 32ull * oA, startB = stB + 32ull * oB;
     uint32_t nblk = (kmaxA > kmaxB ? kmaxA : kmaxB) + 2;
     uint32_t V = VBASE;
-    uint32_t snap = 0;  // SPL: B's metric half at the end of its warm-up (high), A's at chunk block rs-1 (low)
+    // SPL: kept vectors, one per half: sv1 = (A's end, B's start), sv2 = (A's start, B's end) (low, high)
+    uint32_t sv1 = 0, sv2 = 0;
     uint32_t kb = 0;
     uint32_t tbn = LL::TBS - (blockIdx.x & 3u);  // staggered first traceback batches
     __amdgpu_buffer_rsrc_t rsA = tg_rsrc<CH>(in, startA, availB), rsB = tg_rsrc<CH>(in, startB, availB);
@@ -276,10 +294,11 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(SPL
             wA = ~wA;
             wB = ~wB;
         }
-        if constexpr (SPL) {
-            // block ends: B's warm-up end (block kPkWarm - 1) into the high half, A's block rs - 1 into the low
-            if (j == kPkWarm - 1) snap = V;
-            if (j == rs - 1) snap = __builtin_amdgcn_perm(snap, V, 0x07060100u);
+        if constexpr (SPL) {  // kept vectors (block ends: renormalised, fields cleared)
+            if (j == seA) sv1 = __builtin_amdgcn_perm(sv1, V, 0x07060100u);  // low half from V
+            if (j == ssB) sv1 = __builtin_amdgcn_perm(V, sv1, 0x07060100u);  // high half from V
+            if (j == ssA) sv2 = __builtin_amdgcn_perm(sv2, V, 0x07060100u);
+            if (j == seB) sv2 = __builtin_amdgcn_perm(V, sv2, 0x07060100u);
         }
         wave_sync();
         if (j >= 1) {
@@ -290,10 +309,10 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(SPL
             wave_sync();
             const uint32_t nw = j - 1 - kb;
             const uint32_t k = kb + tbl;
-            if (tbl < nw && k >= (tbB ? kminB : 0u) && k < (tbB ? kmaxB : kmaxA)) {
+            if (tbl < nw && k >= (tbB ? kminB : kminA) && k < (tbB ? kmaxB : kmaxA)) {
                 const TbC tc = tb_direct<(J < 6 ? 6 : J), CORE == B32>((int)k);
                 const uint32_t w = traceback_word_tg<J, CORE == B32>(tbring, (tbl + 1u) * 256u, tc);
-                const uint32_t kc = k + (tbB ? koffB : 0u);  // chunk word
+                const uint32_t kc = k + (tbB ? oB : oA);  // chunk word
                 if constexpr (OB == 32) {
                     ((uint32_t*)out)[tbStart + kc] = w;
                 } else {
@@ -331,8 +350,8 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(SPL
     const int r6a = sA % 6, r6b = sB % 6;
     using P0 = std::integral_constant<int, 0>;
     using P1 = std::integral_constant<int, 1>;
-    for (int pass = 0;; pass++) {
-        for (uint32_t j = 0;; j += 3) {
+    for (uint32_t pass = 0;; pass++) {
+        for (uint32_t j = 0; nblk; j += 3) {
             put_row(P0{}, rAA, rAB, sA, r6a);
             if (lane < 32) put_row(P1{}, rBA, rBB, sB, r6b);
             rsA = tg_rsrc<CH>(in, startA + 32ull * (j + 3), availB);
@@ -350,26 +369,68 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(SPL
             wave_sync();
         }
         if constexpr (!SPL) break;
-        // SPL: B's words are exact when its vector equals A's at chunk block rs - 1 in every lane
-        if (pass == 1 || __builtin_amdgcn_ballot_w64((snap & 0xFFFFu) != (snap >> 16)) == 0) break;
-        if (lane == 0 && geo.stats) atomicAdd(geo.stats, 1u);  // counted like a segment re-decode
-        // re-decode B's words rs .. W-1 from chunk block rs with A's vector, in both halves (A writes nothing)
-        V = (snap & 0xFFFFu) * 65537u;
-        startA = startB = crA.startWord * (uint64_t)OB + 32ull * rs;
-        kmaxA = 0;
-        kminB = 0;
-        kmaxB = WA - rs;
-        koffB = rs;
-        nblk = kmaxB + 2;
+        // SPL: the left neighbours' end vectors: B's is A's (sv1 low); A's is the previous wave's B end
+        // (tail workgroups, through the waves' table LDS after a barrier)
+        uint32_t nb = 0;
+        if (tail) {
+            __syncthreads();
+            wlds[LL::TAB_OFF + lane] = sv2;
+            __syncthreads();
+            if (wv > 0) nb = lds[(wv - 1) * LL::WAVE + LL::TAB_OFF + lane];
+            __syncthreads();
+        }
+        const bool mA = pA > 0 && __builtin_amdgcn_ballot_w64((sv2 & 0xFFFFu) != (nb >> 16)) != 0;
+        const bool mB = __builtin_amdgcn_ballot_w64((sv1 >> 16) != (sv1 & 0xFFFFu)) != 0;
+        const bool more = tail ? __syncthreads_or(mA || mB) != 0 : (mA || mB);
+        if (!more || pass + 1u >= 2u * P) break;  // WG-uniform; after P passes no start differs
+        if (lane == 0 && geo.stats && (mA || mB)) atomicAdd(geo.stats, (mA ? 1u : 0u) + (mB ? 1u : 0u));
+        // decode again every part whose start vector differs, from block cut(p) with the left end vector;
+        // an idle half repeats the other half's job without writing or keeping vectors
+        uint32_t vA = 0, vB = 0;
+        if (mA) {
+            oA = pk_cut(pA, P, WA);
+            kminA = 0;
+            kmaxA = pk_cut(pA + 1u, P, WA) - oA;
+            ssA = ~0u;
+            seA = kmaxA - 1u;
+            vA = nb >> 16;
+            sv2 = __builtin_amdgcn_perm(sv2, vA, 0x07060100u);  // its start vector
+        }
+        if (mB) {
+            oB = pk_cut(pB, P, WA);
+            kminB = 0;
+            kmaxB = pk_cut(pB + 1u, P, WA) - oB;
+            ssB = ~0u;
+            seB = pB + 1u < P ? kmaxB - 1u : ~0u;
+            vB = sv1 & 0xFFFFu;
+            sv1 = __builtin_amdgcn_perm(vB << 16, sv1, 0x07060100u);
+        }
+        if (!mA) {  // idle A: B's job (or nothing)
+            oA = oB;
+            kminA = kmaxA = 0;
+            ssA = seA = ~0u;
+            vA = vB;
+        }
+        if (!mB) {
+            oB = oA;
+            kminB = kmaxB = 0;
+            ssB = seB = ~0u;
+            vB = vA;
+        }
+        V = vA | vB << 16;
+        nblk = mA || mB ? (mA ? kmaxA : kmaxB) + 2u : 0u;
+        if (mA && mB && kmaxB > kmaxA) nblk = kmaxB + 2u;
+        startA = stA + 32ull * oA;
+        startB = stB + 32ull * oB;
         kb = 0;
         tbn = LL::TBS - (blockIdx.x & 3u);
         wave_sync();
         rsA = tg_rsrc<CH>(in, startA, availB);
-        rsB = rsA;
+        rsB = tg_rsrc<CH>(in, startB, availB);
         rAA = IN::template load<0>(rsA, vo1);
         rBA = IN::template load<0>(rsA, vo2);
-        rAB = rAA;
-        rBB = rBA;
+        rAB = IN::template load<0>(rsB, vo1);
+        rBB = IN::template load<0>(rsB, vo2);
     }
     fair.end(lane);
     if (geo.check) {

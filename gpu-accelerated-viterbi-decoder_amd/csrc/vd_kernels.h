@@ -55,6 +55,9 @@ struct Geom {
     // of batch c / nchunks
     uint32_t nbatch = 1;
     uint64_t inStride = 0, outStride = 0;
+    // vd_decode_pk split launches: workgroups from tailWG on decode one chunk each (chunk 4 tailWG + g -
+    // tailWG) with their 4 waves (vd_kernel_pk.h "split"); ~0u = none
+    uint32_t tailWG = ~0u;
 };
 // Progress board of the fairness controller: per SIMD slot (XCC, SE, SH, CU, SIMD from the hardware
 // wave id) kFairWaves 32-bit words, one per hardware wave slot of that SIMD (HW_ID.WAVE_ID): the blocks

@@ -100,8 +100,10 @@ def _single(gpu, opt, packed_t, nin, n, env):
 def test_packed_split_single_launch(gpu, vo, opt, nbits, snr):
     """Single-batch launches on vd_decode_pk's split kernel (one chunk per wave, cut at a multiple of 3 blocks,
     the second part started 6 blocks early and checked at the cut): equal to vd_decode_tg's segment launch
-    (VD_PK_SPLIT=0), to the unsplit launch (VD_NO_SPLIT=1) and to the oracle.  13.1M bits: 64 words per chunk
-    (the smallest split); 9M bits: below it (not split)."""
+    (VD_PK_SPLIT=0), to the unsplit launch (VD_NO_SPLIT=1), to the split launch without tail workgroups
+    (VD_PK_TAIL=0) and to the oracle.  With 6400 chunks on 1024 SIMDs the last 256 chunks go to tail
+    workgroups (8 parts over 4 waves, checks across waves).  13.1M bits: 64 words per chunk (the smallest
+    split); 9M bits: below it (not split)."""
     n = 2 * nbits
     packed, stride, nin = _batches(gpu, opt, nbits, snr, 1, 91)
     before = gpu.split_redecodes()
@@ -109,12 +111,13 @@ def test_packed_split_single_launch(gpu, vo, opt, nbits, snr):
     redec = gpu.split_redecodes() - before
     tg = _single(gpu, opt, packed, nin, n, {"VD_PK_SPLIT": "0"})
     whole = _single(gpu, opt, packed, nin, n, {"VD_NO_SPLIT": "1"})
+    notail = _single(gpu, opt, packed, nin, n, {"VD_PK_TAIL": "0"})
     p = packed[:nin].cpu().numpy().view(np.int32)
     ref, ok = vo.decode(opt, p, input_num=n, nthreads=16)
     got = pk.cpu().numpy().view(ref.dtype)
     bad = np.flatnonzero(got != ref)
     assert bad.size == 0, f"{bad.size} of {ref.size} words differ (re-decoded: {redec}), first {bad[:5]}"
-    assert torch.equal(pk, tg) and torch.equal(pk, whole)
+    assert torch.equal(pk, tg) and torch.equal(pk, whole) and torch.equal(pk, notail)
 
 
 @pytest.mark.gpu
@@ -137,3 +140,5 @@ def test_packed_split_random_input_redecodes(gpu, vo, opt):
     bad = np.flatnonzero(got != ref)
     assert bad.size == 0, f"{bad.size} of {ref.size} words differ (re-decoded: {redec}), first {bad[:5]}"
     assert redec > 0, redec
+    notail = _single(gpu, opt, packed, nin, n, {"VD_PK_TAIL": "0"})
+    assert torch.equal(pk, notail)
