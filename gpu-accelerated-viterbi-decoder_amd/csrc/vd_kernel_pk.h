@@ -116,7 +116,8 @@ __host__ __device__ constexpr uint32_t pk_cut(uint32_t p, uint32_t P, uint32_t W
     return p == 0 ? 0u : p >= P ? W : 6u + 3u * ((2u * p * (W - 6u) + 3u * P) / (6u * P));
 }
 
-template <int CH, int CORE, int OB = 32, bool SPL = false, int NW = 8>
+// NW, ABL: tools only (waves per SIMD of the LDS layout; component ablations as vd_decode_tg's, wrong outputs)
+template <int CH, int CORE, int OB = 32, bool SPL = false, int NW = 8, int ABL = 0>
 __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(SPL ? 7 : NW))) void vd_decode_pk(const void* __restrict__ in_all, void* __restrict__ out_all, Geom geo)
 {
     using IN = TgIn<CH>;
@@ -198,10 +199,21 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(SPL
     // SPL: kept vectors, one per half: sv1 = (A's end, B's start), sv2 = (A's start, B's end) (low, high)
     uint32_t sv1 = 0, sv2 = 0;
     uint32_t kb = 0;
+    uint32_t sink = 0;  // kAblNoStores
     uint32_t tbn = LL::TBS - (blockIdx.x & 3u);  // staggered first traceback batches
     __amdgpu_buffer_rsrc_t rsA = tg_rsrc<CH>(in, startA, availB), rsB = tg_rsrc<CH>(in, startB, availB);
     typename IN::raw_t rAA = IN::template load<0>(rsA, vo1), rBA = IN::template load<0>(rsA, vo2);
     typename IN::raw_t rAB = IN::template load<0>(rsB, vo1), rBB = IN::template load<0>(rsB, vo2);
+    // kAblLoad2: the next group's words too (loads two groups ahead)
+    constexpr bool LD2 = (ABL & kAblLoad2) != 0;
+    typename IN::raw_t nAA{}, nBA{}, nAB{}, nBB{};
+    if constexpr (LD2) {
+        const __amdgpu_buffer_rsrc_t qA = tg_rsrc<CH>(in, startA + 96ull, availB), qB = tg_rsrc<CH>(in, startB + 96ull, availB);
+        nAA = IN::template load<0>(qA, vo1);
+        nBA = IN::template load<0>(qA, vo2);
+        nAB = IN::template load<0>(qB, vo1);
+        nBB = IN::template load<0>(qB, vo2);
+    }
     // traceback roles: lanes 0..31 trace half A's words, 32..63 half B's
     const bool tbB = lane >= 32;
     const uint32_t tbl = (uint32_t)(lane & 31);
@@ -217,7 +229,7 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(SPL
     auto issue = [&](auto Rc) {
         constexpr int r = decltype(Rc)::value;
         constexpr int K = r % 6;
-        if constexpr ((r / 6) % 2 == 0) vp[r] = *(lptr)(tl + aK[K] + TT::row(r));
+        if constexpr ((r / 6) % 2 == 0 && !(ABL & kAblNoTabReads)) vp[r] = *(lptr)(tl + aK[K] + TT::row(r));
     };
     auto block = [&](auto PHc, uint32_t j) {
         constexpr int PH = decltype(PHc)::value;
@@ -232,13 +244,13 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(SPL
             constexpr int r = 32 * BB + i;
             constexpr bool ODD = (r / 6) % 2 == 1;
             constexpr int RP = ODD ? r - 6 : r;
-            const uint32_t m = ODD ? vp[RP].y : vp[RP].x;
+            const uint32_t m = (ABL & kAblNoTabReads) ? (uint32_t)aK[K] : ODD ? vp[RP].y : vp[RP].x;
             if constexpr (Q <= 3) pk_stage_dpp<Q>(V, m);
             else if constexpr (Q == 4) pk_stage_lds_pre<false>(V, m, pa5);
             else if constexpr (ALT) pk_stage_lds_post(V, m, pa5);
             else pk_stage_lds_pre<true>(V, m, pa5);
             if constexpr (r + TGD < 96) issue(std::integral_constant<int, r + TGD>{});
-            if constexpr (i % J == J - 1) {
+            if constexpr (i % J == J - 1 && !(ABL & kAblNoReadout)) {
                 // field read-out, both chunks, then both fields cleared; at the block end the renormalisation
                 // on the whole word (vd_decode_tg)
                 constexpr int g = (i % 32) / J;
@@ -309,11 +321,13 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(SPL
             wave_sync();
             const uint32_t nw = j - 1 - kb;
             const uint32_t k = kb + tbl;
-            if (tbl < nw && k >= (tbB ? kminB : kminA) && k < (tbB ? kmaxB : kmaxA)) {
+            if (!(ABL & kAblNoTraceback) && tbl < nw && k >= (tbB ? kminB : kminA) && k < (tbB ? kmaxB : kmaxA)) {
                 const TbC tc = tb_direct<(J < 6 ? 6 : J), CORE == B32>((int)k);
                 const uint32_t w = traceback_word_tg<J, CORE == B32>(tbring, (tbl + 1u) * 256u, tc);
                 const uint32_t kc = k + (tbB ? oB : oA);  // chunk word
-                if constexpr (OB == 32) {
+                if constexpr (ABL & kAblNoStores) {
+                    sink ^= w + kc;
+                } else if constexpr (OB == 32) {
                     ((uint32_t*)out)[tbStart + kc] = w;
                 } else {
                     uint16_t* const o = (uint16_t*)out + tbStart;
@@ -352,14 +366,29 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(SPL
     using P1 = std::integral_constant<int, 1>;
     for (uint32_t pass = 0;; pass++) {
         for (uint32_t j = 0; nblk; j += 3) {
-            put_row(P0{}, rAA, rAB, sA, r6a);
-            if (lane < 32) put_row(P1{}, rBA, rBB, sB, r6b);
-            rsA = tg_rsrc<CH>(in, startA + 32ull * (j + 3), availB);
-            rsB = tg_rsrc<CH>(in, startB + 32ull * (j + 3), availB);
-            rAA = IN::template load<0>(rsA, vo1);
-            rBA = IN::template load<0>(rsA, vo2);
-            rAB = IN::template load<0>(rsB, vo1);
-            rBB = IN::template load<0>(rsB, vo2);
+            if constexpr (!(ABL & kAblNoTabBuild)) {
+                put_row(P0{}, rAA, rAB, sA, r6a);
+                if (lane < 32) put_row(P1{}, rBA, rBB, sB, r6b);
+            }
+            if constexpr (LD2) {
+                rAA = nAA;
+                rBA = nBA;
+                rAB = nAB;
+                rBB = nBB;
+                rsA = tg_rsrc<CH>(in, startA + 32ull * (j + 6), availB);
+                rsB = tg_rsrc<CH>(in, startB + 32ull * (j + 6), availB);
+                nAA = IN::template load<0>(rsA, vo1);
+                nBA = IN::template load<0>(rsA, vo2);
+                nAB = IN::template load<0>(rsB, vo1);
+                nBB = IN::template load<0>(rsB, vo2);
+            } else if constexpr (!(ABL & kAblNoLoads)) {
+                rsA = tg_rsrc<CH>(in, startA + 32ull * (j + 3), availB);
+                rsB = tg_rsrc<CH>(in, startB + 32ull * (j + 3), availB);
+                rAA = IN::template load<0>(rsA, vo1);
+                rBA = IN::template load<0>(rsA, vo2);
+                rAB = IN::template load<0>(rsB, vo1);
+                rBB = IN::template load<0>(rsB, vo2);
+            }
             if ((j / 3) % 2 == 0) fair.group(j, 3u, lane);
             wave_sync();
             sfor<TGD>([&](auto X) { issue(X); });
@@ -431,8 +460,18 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(SPL
         rBA = IN::template load<0>(rsA, vo2);
         rAB = IN::template load<0>(rsB, vo1);
         rBB = IN::template load<0>(rsB, vo2);
+        if constexpr (LD2) {
+            const __amdgpu_buffer_rsrc_t qA = tg_rsrc<CH>(in, startA + 96ull, availB), qB = tg_rsrc<CH>(in, startB + 96ull, availB);
+            nAA = IN::template load<0>(qA, vo1);
+            nBA = IN::template load<0>(qA, vo2);
+            nAB = IN::template load<0>(qB, vo1);
+            nBB = IN::template load<0>(qB, vo2);
+        }
     }
     fair.end(lane);
+    if constexpr ((ABL & kAblNoStores) != 0) {
+        if (sink == 0x9E3779B9u) ((uint32_t*)out)[lane] = sink;  // keeps the traceback live
+    }
     if (geo.check) {
         wave_sync();
         const bool bad = lane < 3 * kGuardWords && wlds[LL::guard(lane)] != kGuardPattern;

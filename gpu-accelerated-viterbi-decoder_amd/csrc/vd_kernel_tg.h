@@ -54,6 +54,10 @@ constexpr int kAblX32Perm = 16384, kAblX16Perm = 32768;
 constexpr int kAblIntMax = 65536;
 // latency studies (tools): table reads 8 stages ahead instead of 4; fairness controller every 4th group head
 constexpr int kAblTgd8 = 131072, kAblFair4 = 262144;
+// vd_decode_pk study: trace back but keep the words in a register (no output stores)
+constexpr int kAblNoStores = 524288;
+// vd_decode_pk study: input loads two groups ahead (a second register set) instead of one
+constexpr int kAblLoad2 = 1048576;
 constexpr int kAblAcsOnly = kAblNoTraceback | kAblNoTabReads | kAblNoReadout | kAblNoTabBuild | kAblNoLoads;
 
 template <int CH>

@@ -17,6 +17,7 @@
 #include "../gpu-accelerated-viterbi-decoder_amd/csrc/vd_segplan.h"
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP error %s at %d\n", hipGetErrorString(e), __LINE__); exit(1); } } while (0)
 using KFn = void (*)(const void*, void*, vd::Geom);
+#define PK(A) (KFn)vd::vd_decode_pk<vd::HARD, vd::B32, 32, false, 8, (A)>
 
 template <int ABL>
 struct V {
@@ -27,12 +28,10 @@ struct V {
 struct Variant { const char* name; KFn hard, soft8; int seg = vd::kSegPieces; uint32_t warm = vd::kSplitWarm; KFn hardBatched = nullptr; };
 #ifndef VD_ABX_VARIANTS
 #define VD_ABX_VARIANTS                                                                                      \
-    {"vd_decode_pk, 8 waves/SIMD (TBS 5)", V<0>::hard, V<0>::soft8, vd::kSegPieces, vd::kSplitWarm,          \
-     (KFn)vd::vd_decode_pk<vd::HARD, vd::B32>},                                                             \
-    {"vd_decode_pk, 7 waves/SIMD (TBS 6)", V<0>::hard, V<0>::soft8, vd::kSegPieces, vd::kSplitWarm,          \
-     (KFn)vd::vd_decode_pk<vd::HARD, vd::B32, 32, false, 7>},                                               \
-    {"vd_decode_pk, 6 waves/SIMD (TBS 8)", V<0>::hard, V<0>::soft8, vd::kSegPieces, vd::kSplitWarm,          \
-     (KFn)vd::vd_decode_pk<vd::HARD, vd::B32, 32, false, 6>},
+    {"vd_decode_pk full", V<0>::hard, V<0>::soft8, vd::kSegPieces, vd::kSplitWarm, PK(0)},                  \
+    {"pk -traceback", V<0>::hard, V<0>::soft8, vd::kSegPieces, vd::kSplitWarm, PK(vd::kAblNoTraceback)},     \
+    {"pk -loads", V<0>::hard, V<0>::soft8, vd::kSegPieces, vd::kSplitWarm, PK(vd::kAblNoLoads)},             \
+    {"pk loads two groups ahead", V<0>::hard, V<0>::soft8, vd::kSegPieces, vd::kSplitWarm, PK(vd::kAblLoad2)},
 #endif
 
 static double median(std::vector<float> v)
