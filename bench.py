@@ -5,7 +5,9 @@ One step = one pass of the decode hot path over one batch of each headline workl
 already resident in HBM:
   * HARD  input, M_B32 option       (BASELINE configs[1]: 32M bits, `-i h -m b32`)
   * SOFT8 input, M_B16 option       (BASELINE configs[2]: 32M bits, `-i s8 -m b16`)
-both on the fp32 exact-integer tagged core, which reproduces each option's tie rule.
+HARD batches on vd_decode_pk (exact-integer tagged metrics in the int16 halves of one word, two chunks
+per wave: 32-bit add, DPP subtract, v_pk_max_u16), SOFT8 batches on vd_decode_tg (the fp32 exact-integer
+tagged core); both reproduce each option's tie rule word for word.
 value = decoded bits of both batches (2 x getMessageLen(64e6) = 63,999,872) / step time, summed
 over ranks.  Multi-GPU (BASELINE configs[3]): one process per GPU, each rank decodes its own
 independent batches (weak scaling, no data-path collective; an RCCL all_gather of per-rank
@@ -806,15 +808,17 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "fp32 exact-integer (int32/int16 tie semantics)",
+            "dtype": "exact integers: HARD in int16 halves (u16x2), SOFT8 in fp32 (int32/int16 tie semantics)",
             "data": f"synthetic: the reference harness chain generated on the GPU bit-exactly (std::mt19937 "
                     f"bits, K=7 (0171,0133) encoder, BPSK + normal_distribution<float> AWGN at {SNR_DB} dB, "
                     f"quantiser scale 40000), seeds (1+2i, 2+2i) for batch i = 2 rank + workload",
             "config": {
                 "workload": "per GPU per step: one 32M-bit HARD batch with the M_B32 option (int32 tie rule) + "
                             "one 32M-bit SOFT8 batch with the M_B16 option (int16 tie rule), BASELINE configs[1]+[2], "
-                            "both on the fp32 exact-integer tagged core (not a V_PK int16x2 core: DESIGN.md 4 "
-                            "'Packed int16'); each batch uses the reference's 6400-chunk partition",
+                            "HARD on vd_decode_pk (exact-integer tagged metrics in the int16 halves of one word, "
+                            "two chunks per wave: v_add_u32, v_sub_u32_dpp, v_pk_max_u16), SOFT8 on vd_decode_tg "
+                            "(fp32 exact-integer tagged core; SOFT8's metric spread does not fit int16 halves with "
+                            "history tags: DESIGN.md 4); each batch uses the reference's 6400-chunk partition",
                 "n_bits_per_batch": N_BITS,
                 "decoded_bits_per_batch": batches[0]["msg"],
                 "parallelism": f"batch-shard x{world}" if world > 1 else "single GPU (1-rank RCCL group)",
