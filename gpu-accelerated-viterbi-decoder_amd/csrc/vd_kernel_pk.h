@@ -1,6 +1,7 @@
-// vd_kernel_pk.h -- vd_decode_pk<CH, CORE, OB>: HARD, SOFT4 or FP32 input, TWO chunks per wave, one in each
-// 16-bit half of the lane's metric word (batched launches).  Same decode as vd_decode_tg<CH, CORE, OB> word
-// for word (reference viterbi_core, src/viterbi/viterbi.cu:144-207; tie rules viterbiACS.cuh:113-157,216-256).
+// vd_kernel_pk.h -- vd_decode_pk<CH, CORE, OB, SPL>: HARD, SOFT4 or FP32 input, two trellis chains per
+// wave, one in each 16-bit half of the lane's metric word: two chunks (batched launches) or two parts of one
+// chunk (SPL: single-batch split launches, below).  Same decode as vd_decode_tg<CH, CORE, OB> word for word
+// (reference viterbi_core, src/viterbi/viterbi.cu:144-207; tie rules viterbiACS.cuh:113-157,216-256).
 //
 // Why it is exact.  A HARD metric needs few bits: every path metric lies within D = 12 units of the best
 // one and the best grows by at most 1 unit per stage, so between two renormalisations (32 stages) the
@@ -21,8 +22,8 @@
 // v_add_u32 + v_pk_max_u16 with one crossbar round trip for both chunks; renormalisation is the int32
 // kernels' readfirstlane / s_sub / v_subrev on the whole word (again a homomorphism).
 //
-// The two chunks of a wave are consecutive chunks 2w, 2w+1 of the launch (the same batch: 6400 is even);
-// they decode in lockstep over the longer one's blocks, each emitting only its own words.  LDS per wave:
+// Batched: the two chunks of a wave are consecutive chunks 2w, 2w+1 of the launch (the same batch: 6400 is
+// even); they decode in lockstep over the longer one's blocks, each emitting only its own words.  LDS per wave:
 // [guard | label-region table with the +tag area (TgTabLT<true>) | guard | ring A | ring B | guard]; two
 // rings in a wave's 5,120 B leave 6 slots each, so a traceback batch traces 5 words per chunk, both chunks'
 // words in one pass (lanes 0..4 chunk A, lanes 32..36 chunk B).
