@@ -136,15 +136,20 @@ launch_fn pick_pk_ob(int o)
 {
     return out_of(o) == 1 ? pick_pk_core<CH, 16, SPL>(met_of(o)) : pick_pk_core<CH, 32, SPL>(met_of(o));
 }
-template <bool SPL>
-launch_fn pick_pk(int o)
+template <bool SPL, int L>
+launch_fn pick_pk_ch(int o)
 {
     switch (ch_of(o)) {
-    case 0: return pick_pk_ob<vd::HARD, SPL>(o);
-    case 1: return pick_pk_ob<vd::SOFT4, SPL>(o);
-    case 4: return pick_pk_ob<vd::FP32, SPL>(o);
+    case 0: return pick_pk_ob<L + vd::HARD, SPL>(o);
+    case 1: return pick_pk_ob<L + vd::SOFT4, SPL>(o);
+    case 4: return pick_pk_ob<L + vd::FP32, SPL>(o);
     }
     return nullptr;
+}
+template <bool SPL>
+launch_fn pick_pk(int o, bool llr)
+{
+    return llr ? pick_pk_ch<SPL, vd::kLlr>(o) : pick_pk_ch<SPL, 0>(o);
 }
 
 template <int L>
@@ -172,25 +177,25 @@ const char* kname(int o)
 {
     static const char* names[5][3] = {
         {"vd_decode_pk<HARD,B32> (int16 halves: batched, two chunks per lane; single batch, one chunk cut in two) / "
-         "vd_decode_tg<HARD,B32> (single batches with chunks under 64 words; fused LLR); M_B32 tie rule",
+         "vd_decode_tg<HARD,B32> (single batches with chunks under 64 words); M_B32 tie rule",
          "vd_decode_pk<HARD,B16> (int16 halves: batched, two chunks per lane; single batch, one chunk cut in two) / "
-         "vd_decode_tg<HARD,B16> (single batches with chunks under 64 words; fused LLR); M_B16 tie rule",
+         "vd_decode_tg<HARD,B16> (single batches with chunks under 64 words); M_B16 tie rule",
          "vd_decode_pk<HARD,F16> (int16 halves: batched, two chunks per lane; single batch, one chunk cut in two) / "
-         "vd_decode_tg<HARD,F16> (single batches with chunks under 64 words; fused LLR); M_FP16 tie rule"},
+         "vd_decode_tg<HARD,F16> (single batches with chunks under 64 words); M_FP16 tie rule"},
         {"vd_decode_pk<SOFT4,B32> (int16 halves: batched, two chunks per lane; single batch, one chunk cut in two) / "
-         "vd_decode_tg<SOFT4,B32> (single batches with chunks under 64 words; fused LLR); M_B32 tie rule",
+         "vd_decode_tg<SOFT4,B32> (single batches with chunks under 64 words); M_B32 tie rule",
          "vd_decode_pk<SOFT4,B16> (int16 halves: batched, two chunks per lane; single batch, one chunk cut in two) / "
-         "vd_decode_tg<SOFT4,B16> (single batches with chunks under 64 words; fused LLR); M_B16 tie rule",
+         "vd_decode_tg<SOFT4,B16> (single batches with chunks under 64 words); M_B16 tie rule",
          "vd_decode_pk<SOFT4,F16> (int16 halves: batched, two chunks per lane; single batch, one chunk cut in two) / "
-         "vd_decode_tg<SOFT4,F16> (single batches with chunks under 64 words; fused LLR); M_FP16 tie rule"},
+         "vd_decode_tg<SOFT4,F16> (single batches with chunks under 64 words); M_FP16 tie rule"},
         {"vd_decode_tg<SOFT8,B32> (fp32 tagged core, M_B32 tie rule)", "vd_decode_tg<SOFT8,B16> (fp32 tagged core, M_B16 tie rule)", "-"},
         {"vd_decode_tg<SOFT16,B32> (int32 tagged patterns, M_B32 tie rule)", "-", "-"},
         {"vd_decode_pk<FP32,B32> (int16 halves: batched, two chunks per lane; single batch, one chunk cut in two) / "
-         "vd_decode_tg<FP32,B32> (single batches with chunks under 64 words; fused LLR); M_B32 tie rule",
+         "vd_decode_tg<FP32,B32> (single batches with chunks under 64 words); M_B32 tie rule",
          "vd_decode_pk<FP32,B16> (int16 halves: batched, two chunks per lane; single batch, one chunk cut in two) / "
-         "vd_decode_tg<FP32,B16> (single batches with chunks under 64 words; fused LLR); M_B16 tie rule",
+         "vd_decode_tg<FP32,B16> (single batches with chunks under 64 words); M_B16 tie rule",
          "vd_decode_pk<FP32,F16> (int16 halves: batched, two chunks per lane; single batch, one chunk cut in two) / "
-         "vd_decode_tg<FP32,F16> (single batches with chunks under 64 words; fused LLR); M_FP16 tie rule"},
+         "vd_decode_tg<FP32,F16> (single batches with chunks under 64 words); M_FP16 tie rule"},
     };
     if (!valid(o)) return "-";
     return names[ch_of(o)][met_of(o)];
@@ -344,7 +349,7 @@ static int launch_decode(const vd_decoder* d, const void* in_d, void* out_d, siz
     g.nbatch = nbatch;
     g.inStride = inStride;
     g.outStride = outStride;
-    launch_fn fp = nbatch > 1 && !llr && d->pk && g.nchunks % (2 * vd::kWaves) == 0 ? pick_pk<false>(options) : nullptr;
+    launch_fn fp = nbatch > 1 && d->pk && g.nchunks % (2 * vd::kWaves) == 0 ? pick_pk<false>(options, llr) : nullptr;
     if (fp) {  // two chunks per wave: nchunks * nbatch / 8 workgroups
         fp(in_d, out_d, g, (unsigned)((uint64_t)g.nchunks * nbatch / (2 * vd::kWaves)), s);
         VD_HIP(hipGetLastError());
@@ -352,8 +357,8 @@ static int launch_decode(const vd_decoder* d, const void* in_d, void* out_d, siz
     }
     // single batch, chunks long enough to cut: one chunk per wave, cut in two halves (nchunks / 4 workgroups)
     const uint64_t w32 = out_of(options) != 0 ? g.packNum / 2 : g.packNum;
-    fp = nbatch == 1 && !llr && d->pk && d->pksplit && d->split && g.nchunks % vd::kWaves == 0 &&
-                 w32 / g.nchunks >= (uint64_t)vd::kSplitMinWords ? pick_pk<true>(options) : nullptr;
+    fp = nbatch == 1 && d->pk && d->pksplit && d->split && g.nchunks % vd::kWaves == 0 &&
+                 w32 / g.nchunks >= (uint64_t)vd::kSplitMinWords ? pick_pk<true>(options, llr) : nullptr;
     if (fp) {
         g.stats = d->ds->stats;
         // the last nchunks mod (SIMDs) chunks one per workgroup of 4 waves (8 parts each): with 6400 chunks

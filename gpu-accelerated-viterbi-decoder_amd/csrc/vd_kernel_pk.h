@@ -72,13 +72,15 @@ __device__ __forceinline__ void pk_stage_lds_post(uint32_t& V, uint32_t m, int p
         : "+{v60}"(V), "=&v"(a), "=&v"(b) : "v"(m), "v"(vp));
 }
 
-// metric format per input: history field length J, scale 2^S, base of a half
+// metric format per input (CH >= kLlr: float channel values quantised in the table build as for the base
+// format, vd_kernel_tg.h TgInLlr): history field length J, scale 2^S, base of a half
 template <int CH>
 struct PkFmt {
-    static constexpr int J = CH == HARD ? 8 : 4;
+    static constexpr int B = CH & 7;
+    static constexpr int J = B == HARD ? 8 : 4;
     static constexpr int S = J + 1;
-    static constexpr uint32_t BASE = CH == HARD ? 16384u : 8192u;
-    static_assert(CH == HARD || CH == SOFT4 || CH == FP32, "int16 halves hold HARD, SOFT4 and FP32 metrics");
+    static constexpr uint32_t BASE = B == HARD ? 16384u : 8192u;
+    static_assert(B == HARD || B == SOFT4 || B == FP32, "int16 halves hold HARD, SOFT4 and FP32 metrics");
 };
 
 // LDS layout of a wave (words), for NW resident workgroups (waves per SIMD) per CU
@@ -350,8 +352,8 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(SPL
         constexpr int part = decltype(PT)::value;
         const int32_t tg = part ? tg0B : tg0A;
         int AA, BA, AB, BBv;
-        IN::ab(wa, li, AA, BA, 1.0f);
-        IN::ab(wb, li, AB, BBv, 1.0f);
+        IN::ab(wa, li, AA, BA, geo.scale);
+        IN::ab(wb, li, AB, BBv, geo.scale);
         const int32_t pa = AA + AB * 65536, pb = BA + BBv * 65536;
         auto f = [](int32_t x) { return __builtin_bit_cast(float, x); };
         const int32_t e3 = __mul24(pa, 1 << S) + tg, e2 = __mul24(pb, 1 << S) + tg;

@@ -28,6 +28,20 @@ def channel_values(n, snr, seed):
     return (out + rng.standard_normal(n).astype(np.float32) * sigma).astype(np.float32)
 
 
+def channel_values_fast(n, snr, seed):
+    """channel_values without the Python loop (numpy taps of the same encoder; other random draws)"""
+    rng = np.random.default_rng(seed)
+    b = np.concatenate([np.zeros(6, np.uint8), rng.integers(0, 2, n // 2).astype(np.uint8)])
+    t = np.arange(6, b.size)
+    o0 = b[t] ^ b[t - 1] ^ b[t - 2] ^ b[t - 3] ^ b[t - 6]  # 0171: register bits 6, 5, 4, 3, 0
+    o1 = b[t] ^ b[t - 2] ^ b[t - 3] ^ b[t - 5] ^ b[t - 6]  # 0133: register bits 6, 4, 3, 1, 0
+    out = np.empty(n, dtype=np.float32)
+    out[0::2] = np.where(o0 == 1, 1.0, -1.0)
+    out[1::2] = np.where(o1 == 1, 1.0, -1.0)
+    sigma = np.float32(10.0 ** (-snr / 5.0))
+    return (out + rng.standard_normal(n).astype(np.float32) * sigma).astype(np.float32)
+
+
 def specials():
     """Ties, signed zeros, saturation, the x86 lrintf 'integer indefinite' cases, denormals."""
     v = [0.0, -0.0, 0.5, 1.5, 2.5, -0.5, -1.5, -2.5, 7.5, -8.5, 127.5, -128.5, 128.0, -129.0, 32767.5, -32768.5,
@@ -143,3 +157,27 @@ def test_fused_llr_batch_equals_single(gpu, vd, vo, opt):
         got = out[b * ostride: b * ostride + nout].cpu().numpy().view(refs[b].dtype)
         np.testing.assert_array_equal(got, refs[b])
         assert bool((out[b * ostride + nout: (b + 1) * ostride] == 0xA5).all())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("opt", [HARD | M_B32, SOFT4 | M_B16, FP32 | M_FP16, HARD | M_B16 | O_B16], ids=name)
+def test_fused_llr_split_launch_on_packed_kernel(gpu, vd, vo, opt):
+    """16M bits of float channel values in one fused launch: 78 words per chunk, so HARD / SOFT4 / FP32 run
+    vd_decode_pk's split launch (tail workgroups included) with the packer fused into the table build; equal
+    to the oracle's pack + decode and to the unfused vd_decode_tg path (VD_NO_PK=1)"""
+    import os
+    vals = channel_values_fast(2 * 16_000_000, 1.0, 13)
+    packed = vo.pack(opt, vals, 40000.0)
+    ref, ok = vo.decode(opt, packed, input_num=vals.size, nthreads=16)
+    assert ok
+    with vd.ViterbiCUDA(opt) as d:
+        out, _ = d.run_llr(vals, scale=40000.0)
+    os.environ["VD_NO_PK"] = "1"
+    try:
+        with vd.ViterbiCUDA(opt) as d:
+            tg, _ = d.run_llr(vals, scale=40000.0)
+    finally:
+        del os.environ["VD_NO_PK"]
+    bad = np.flatnonzero(out != ref)
+    assert bad.size == 0, f"{bad.size} words differ, first at {bad[:5]}"
+    assert np.array_equal(tg, ref)
