@@ -106,12 +106,11 @@ int main(int argc, char** argv)
     CK(hipMalloc(&out, (size_t)cus * 8 * 256 * 4));
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
-    // chains per CU: 32 in both (NC 1: 8 workgroups of 4 waves; NC 2: 4 workgroups), the LDS per workgroup
-    // padded so exactly that many fit
-    auto run = [&](int nc) {
-        const int wgPerCu = nc == 1 ? 8 : 4;
-        const size_t lds = 163840 / wgPerCu / 256 * 256;
-        const int grid = cus * wgPerCu;
+    // nc chains per wave, wg workgroups of 4 waves per CU (the LDS per workgroup padded so exactly that many
+    // fit): wg waves per SIMD
+    auto run = [&](int nc, int wg) {
+        const size_t lds = 163840 / wg / 256 * 256;
+        const int grid = cus * wg;
         CK(hipEventRecord(e0));
         if (nc == 1) hipLaunchKernelGGL(chains<1>, dim3(grid), dim3(256), lds, 0, out, groups, tabStride);
         else hipLaunchKernelGGL(chains<2>, dim3(grid), dim3(256), lds, 0, out, groups, tabStride);
@@ -119,15 +118,18 @@ int main(int argc, char** argv)
         CK(hipEventSynchronize(e1));
         float ms;
         CK(hipEventElapsedTime(&ms, e0, e1));
-        // chain-stages per SIMD: 32 chains per CU / 4 SIMDs x 96 groups x stages
-        const double cs = 8.0 * groups * 96;
+        const double cs = (double)wg * nc * groups * 96;  // chain-stages per SIMD
         return ms * 1e6 / cs;
     };
-    for (int i = 0; i < 3; i++) { run(1); run(2); }
-    std::vector<double> a, b;
-    for (int r = 0; r < reps; r++) { a.push_back(run(1)); b.push_back(run(2)); }
-    std::sort(a.begin(), a.end()); std::sort(b.begin(), b.end());
-    printf("ns per chain-stage per SIMD: 1 chain x 8 waves %.3f, 2 chains x 4 waves %.3f\n", a[a.size() / 2], b[b.size() / 2]);
+    const int cfg[][2] = {{1, 8}, {1, 7}, {1, 6}, {2, 8}, {2, 7}, {2, 6}, {2, 4}};
+    for (int i = 0; i < 2; i++)
+        for (auto& c : cfg) run(c[0], c[1]);
+    for (auto& c : cfg) {
+        std::vector<double> a;
+        for (int r = 0; r < reps; r++) a.push_back(run(c[0], c[1]));
+        std::sort(a.begin(), a.end());
+        printf("ns per chain-stage per SIMD: %d chain(s) x %d waves: %.3f\n", c[0], c[1], a[a.size() / 2]);
+    }
     hipFuncAttributes fa;
     CK(hipFuncGetAttributes(&fa, (const void*)chains<1>)); printf("NC 1: %d VGPRs\n", fa.numRegs);
     CK(hipFuncGetAttributes(&fa, (const void*)chains<2>)); printf("NC 2: %d VGPRs\n", fa.numRegs);
