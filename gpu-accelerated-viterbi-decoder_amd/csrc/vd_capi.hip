@@ -151,6 +151,12 @@ launch_fn pick_pk(int o, bool llr)
 {
     return llr ? pick_pk_ch<SPL, vd::kLlr>(o) : pick_pk_ch<SPL, 0>(o);
 }
+// SOFT8 / M_B16 split launches with two fp32 chains per wave (vd_kernel_pk.h F2)
+launch_fn pick_f2(int o)
+{
+    if (ch_of(o) != 2 || met_of(o) != 1) return nullptr;
+    return out_of(o) == 1 ? &launch_pk<vd::SOFT8, 1, 16, true> : &launch_pk<vd::SOFT8, 1, 32, true>;
+}
 
 template <int L>
 launch_fn pick_ch(int o)
@@ -236,6 +242,7 @@ struct vd_decoder {
     int pk = 1;                 // HARD/SOFT4/FP32 launches on vd_decode_pk (VD_NO_PK=1: on vd_decode_tg)
     int pksplit = 1;            // their single-batch launches split on vd_decode_pk (VD_PK_SPLIT=0: tg segments)
     int pktail = 1;             // ... with the tail chunks in 4-wave workgroups (VD_PK_TAIL=0: one chunk per wave)
+    int f2 = 0;                 // SOFT8/M_B16 split launches with two fp32 chains per wave (VD_F2=1; study)
     uint32_t* check = nullptr;  // LDS guard violation counter (vd_set_guard_check), null = off
 };
 
@@ -357,8 +364,10 @@ static int launch_decode(const vd_decoder* d, const void* in_d, void* out_d, siz
     }
     // single batch, chunks long enough to cut: one chunk per wave, cut in two halves (nchunks / 4 workgroups)
     const uint64_t w32 = out_of(options) != 0 ? g.packNum / 2 : g.packNum;
-    fp = nbatch == 1 && d->pk && d->pksplit && d->split && g.nchunks % vd::kWaves == 0 &&
-                 w32 / g.nchunks >= (uint64_t)vd::kSplitMinWords ? pick_pk<true>(options, llr) : nullptr;
+    const bool splitok = nbatch == 1 && d->pk && d->pksplit && d->split && g.nchunks % vd::kWaves == 0 &&
+                         w32 / g.nchunks >= (uint64_t)vd::kSplitMinWords;
+    fp = splitok ? pick_pk<true>(options, llr) : nullptr;
+    if (!fp && splitok && !llr && d->f2) fp = pick_f2(options);
     if (fp) {
         g.stats = d->ds->stats;
         // the last nchunks mod (SIMDs) chunks one per workgroup of 4 waves (8 parts each): with 6400 chunks
@@ -433,6 +442,8 @@ int vd_create(int options, size_t preallocInputNum, int device, vd_decoder** out
     d->pksplit = pks && pks[0] == '0' ? 0 : 1;
     const char* pkt = std::getenv("VD_PK_TAIL");
     d->pktail = pkt && pkt[0] == '0' ? 0 : 1;
+    const char* f2 = std::getenv("VD_F2");
+    d->f2 = f2 && f2[0] == '1' ? 1 : 0;
     const char* chk = std::getenv("VD_CHECK");
     if (chk && chk[0] == '1') {
         int rc = vd_set_guard_check(d, 1);

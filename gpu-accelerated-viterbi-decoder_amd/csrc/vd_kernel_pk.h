@@ -77,17 +77,47 @@ __device__ __forceinline__ void pk_stage_lds_post(uint32_t& V, uint32_t m, int p
 template <int CH>
 struct PkFmt {
     static constexpr int B = CH & 7;
-    static constexpr int J = B == HARD ? 8 : 4;
+    // F2 (SOFT8): two fp32 chains per wave in two registers (vd_decode_tg's tagged fp32 metric each), for
+    // split single-batch launches only -- SOFT8's spread does not fit int16 halves
+    static constexpr bool F2 = B == SOFT8;
+    static constexpr int J = B == HARD || F2 ? 8 : 4;
     static constexpr int S = J + 1;
     static constexpr uint32_t BASE = B == HARD ? 16384u : 8192u;
-    static_assert(B == HARD || B == SOFT4 || B == FP32, "int16 halves hold HARD, SOFT4 and FP32 metrics");
+    static_assert(B == HARD || B == SOFT4 || B == FP32 || F2, "int16 halves hold HARD, SOFT4 and FP32 metrics");
 };
+// F2 stages: vd_decode_tg's tagged fp32 stage on both chains, interleaved (V0, V1 unpinned)
+template <int Q>
+__device__ __forceinline__ void f2_stage_dpp(float& V0, float& V1, float m0, float m1)
+{
+    float a0, a1, b0, b1;
+#define VD_F2_DPP(CTRL)                                                                                      \
+    asm("v_sub_f32 %4, %0, %6\n\tv_sub_f32 %5, %1, %7\n\tv_add_f32 %2, %0, %6\n\tv_add_f32 %3, %1, %7\n\t"       \
+        "v_max_f32_dpp %0, %4, %2 " CTRL " row_mask:0xf bank_mask:0xf\n\t"                                      \
+        "v_max_f32_dpp %1, %5, %3 " CTRL " row_mask:0xf bank_mask:0xf"                                          \
+        : "+v"(V0), "+v"(V1), "=&v"(a0), "=&v"(a1), "=&v"(b0), "=&v"(b1) : "v"(m0), "v"(m1))
+    if constexpr (Q == 0) VD_F2_DPP("quad_perm:[1,0,3,2]");
+    else if constexpr (Q == 1) VD_F2_DPP("quad_perm:[2,3,0,1]");
+    else if constexpr (Q == 2) VD_F2_DPP("row_half_mirror");
+    else VD_F2_DPP("row_ror:8");
+#undef VD_F2_DPP
+}
+template <bool X32>
+__device__ __forceinline__ void f2_stage_lds_pre(float& V0, float& V1, float m0, float m1, int paddr)
+{
+    float a0, a1, b0, b1;
+    asm("v_sub_f32 %0, %2, %3\n\tv_sub_f32 %1, %4, %5" : "=&v"(b0), "=&v"(b1) : "v"(V0), "v"(m0), "v"(V1), "v"(m1));
+    const float p0 = X32 ? tg_partner(b0, paddr) : tg_swz16(b0);
+    const float p1 = X32 ? tg_partner(b1, paddr) : tg_swz16(b1);
+    asm("v_add_f32 %0, %2, %3\n\tv_add_f32 %1, %4, %5" : "=&v"(a0), "=&v"(a1) : "v"(V0), "v"(m0), "v"(V1), "v"(m1));
+    asm("v_max_f32 %0, %1, %2" : "=v"(V0) : "v"(a0), "v"(p0));
+    asm("v_max_f32 %0, %1, %2" : "=v"(V1) : "v"(a1), "v"(p1));
+}
 
 // LDS layout of a wave (words), for NW resident workgroups (waves per SIMD) per CU
-template <int NW = 8>
+template <int NW = 8, bool F2 = false>
 struct PkLds {
     static constexpr int GW = kGuardWords;
-    static constexpr int TAB = TgTabLT<true>::BYTES / 4;
+    static constexpr int TAB = F2 ? 2 * TgTabL::BYTES / 4 : TgTabLT<true>::BYTES / 4;  // F2: a table per chain
     static constexpr int LDSW = 163840 / 4 / (NW * kWaves);                // a wave's share
     static constexpr int TBS = (LDSW - 3 * GW - TAB) / 128 - 1;            // words per traceback batch and chunk
     static constexpr int RING = (TBS + 1) * 64;                            // words per chunk ring
@@ -96,6 +126,7 @@ struct PkLds {
     static __device__ __forceinline__ int guard(int i) { return i < GW ? i : i < 2 * GW ? TAB + i : TAB + 2 * RING + i; }
 };
 static_assert(PkLds<8>::TBS == 5 && kWaves * PkLds<8>::WAVE * 4 <= 20480, "8 workgroups of 4 waves per CU");
+static_assert(PkLds<7, true>::TBS == 3 && kWaves * PkLds<7, true>::WAVE * 4 <= 163840 / 7, "F2: 7 workgroups per CU");
 
 // Split single-batch launches (SPL).  A chunk of W words is cut into P parts at words cut(1) .. cut(P-1),
 // multiples of 3 blocks; part p emits words [cut(p), cut(p+1)).  Part 0 decodes from the chunk start (equal
@@ -120,14 +151,16 @@ __host__ __device__ constexpr uint32_t pk_cut(uint32_t p, uint32_t P, uint32_t W
 }
 
 // NW, ABL: tools only (waves per SIMD of the LDS layout; component ablations as vd_decode_tg's, wrong outputs)
-template <int CH, int CORE, int OB = 32, bool SPL = false, int NW = 8, int ABL = 0>
+template <int CH, int CORE, int OB = 32, bool SPL = false, int NW = (PkFmt<CH>::F2 ? 7 : 8), int ABL = 0>
 __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(SPL ? 7 : NW))) void vd_decode_pk(const void* __restrict__ in_all, void* __restrict__ out_all, Geom geo)
 {
+    constexpr bool F2 = PkFmt<CH>::F2;
+    static_assert(!F2 || (SPL && CORE == B16 && NW == 7), "F2: split launches of the M_B16 core");
     using IN = TgIn<CH>;
-    using TT = TgTabLT<true>;
-    using LL = PkLds<NW>;
+    using TT = std::conditional_t<F2, TgTabL, TgTabLT<true>>;
+    using LL = PkLds<NW, F2>;
     constexpr int J = PkFmt<CH>::J, S = PkFmt<CH>::S;
-    constexpr bool ALT = CORE == B32;  // M_B32: the upper position half takes the +tag entries at phase 0
+    constexpr bool ALT = CORE == B32 && !F2;  // M_B32: the upper position half takes the +tag entries at phase 0
     __shared__ __attribute__((aligned(16))) uint32_t lds[kWaves * LL::WAVE];
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -164,6 +197,7 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(SPL
     const int tagA = 1 << (sA % J), tagB = 1 << (sB % J);
     // entry tag of the row's own class, both halves: tg0 * 65537 (M_FP16: own wins ties, +2^j; else -2^j)
     const int32_t tg0A = (CORE == F16 ? tagA : -tagA) * 65537, tg0B = (CORE == F16 ? tagB : -tagB) * 65537;
+    const float tf0A = -(float)tagA, tf0B = -(float)tagB;  // F2 (M_B16: exchanged wins ties)
     const uint32_t tabl = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)tabb;
     constexpr uint32_t BASE = PkFmt<CH>::BASE;
     constexpr uint32_t VB1 = BASE + (1u << (S - 1));  // a half with metric 0 and a cleared field
@@ -199,11 +233,17 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(SPL
     uint64_t startA = stA + 32ull * oA, startB = stB + 32ull * oB;
     uint32_t nblk = (kmaxA > kmaxB ? kmaxA : kmaxB) + 2;
     uint32_t V = VBASE;
+    // F2: the chains' fp32 metrics (vd_decode_tg: V in [2^23, 2^24), base 1.25 2^23 + 2^(S-1)) and their kept
+    // vectors (bit patterns: A's start / end, B's start / end)
+    constexpr uint32_t VBF = 0x4B200000u + (1u << (S - 1));
+    float V0 = __builtin_bit_cast(float, VBF), V1 = V0;
+    uint32_t kAs = 0, kAe = 0, kBs = 0, kBe = 0;
+    (void)V0, (void)V1, (void)kAs, (void)kAe, (void)kBs, (void)kBe;
     // SPL: kept vectors, one per half: sv1 = (A's end, B's start), sv2 = (A's start, B's end) (low, high)
     uint32_t sv1 = 0, sv2 = 0;
     uint32_t kb = 0;
     uint32_t sink = 0;  // kAblNoStores
-    uint32_t tbn = LL::TBS - (blockIdx.x & 3u);  // staggered first traceback batches
+    uint32_t tbn = LL::TBS - (blockIdx.x & 3u) % LL::TBS;  // staggered first traceback batches
     __amdgpu_buffer_rsrc_t rsA = tg_rsrc<CH>(in, startA, availB), rsB = tg_rsrc<CH>(in, startB, availB);
     typename IN::raw_t rAA = IN::template load<0>(rsA, vo1), rBA = IN::template load<0>(rsA, vo2);
     typename IN::raw_t rAB = IN::template load<0>(rsB, vo1), rBB = IN::template load<0>(rsB, vo2);
@@ -227,12 +267,21 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(SPL
     typedef uint32_t u2v __attribute__((ext_vector_type(2)));
     typedef __attribute__((address_space(3))) const volatile u2v* lptr;
     const __attribute__((address_space(3))) char* tl = (const __attribute__((address_space(3))) char*)tabb;
-    constexpr int TGD = 4;
+    constexpr int TGD = F2 ? 2 : 4;  // table reads ahead (F2: two tables, registers for 2)
     u2v vp[96];
+    typedef __attribute__((address_space(3))) const volatile f2v* lptrf;
+    f2v vf0[96], vf1[96];  // F2: the chains' entry pairs (two tables)
     auto issue = [&](auto Rc) {
         constexpr int r = decltype(Rc)::value;
         constexpr int K = r % 6;
-        if constexpr ((r / 6) % 2 == 0 && !(ABL & kAblNoTabReads)) vp[r] = *(lptr)(tl + aK[K] + TT::row(r));
+        if constexpr (F2) {
+            if constexpr ((r / 6) % 2 == 0) {
+                vf0[r] = *(lptrf)(tl + aK[K] + TT::row(r));
+                vf1[r] = *(lptrf)(tl + TT::BYTES + aK[K] + TT::row(r));
+            }
+        } else if constexpr ((r / 6) % 2 == 0 && !(ABL & kAblNoTabReads)) {
+            vp[r] = *(lptr)(tl + aK[K] + TT::row(r));
+        }
     };
     auto block = [&](auto PHc, uint32_t j) {
         constexpr int PH = decltype(PHc)::value;
@@ -247,11 +296,17 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(SPL
             constexpr int r = 32 * BB + i;
             constexpr bool ODD = (r / 6) % 2 == 1;
             constexpr int RP = ODD ? r - 6 : r;
+            if constexpr (F2) {
+                const float m0 = ODD ? vf0[RP].y : vf0[RP].x, m1 = ODD ? vf1[RP].y : vf1[RP].x;
+                if constexpr (Q <= 3) f2_stage_dpp<Q>(V0, V1, m0, m1);
+                else f2_stage_lds_pre<Q == 5>(V0, V1, m0, m1, pa5);
+            } else {
             const uint32_t m = (ABL & kAblNoTabReads) ? (uint32_t)aK[K] : ODD ? vp[RP].y : vp[RP].x;
             if constexpr (Q <= 3) pk_stage_dpp<Q>(V, m);
             else if constexpr (Q == 4) pk_stage_lds_pre<false>(V, m, pa5);
             else if constexpr (ALT) pk_stage_lds_post(V, m, pa5);
             else pk_stage_lds_pre<true>(V, m, pa5);
+            }
             if constexpr (r + TGD < 96) issue(std::integral_constant<int, r + TGD>{});
             if constexpr (i % J == J - 1 && !(ABL & kAblNoReadout)) {
                 // field read-out, both chunks, then both fields cleared; at the block end the renormalisation
@@ -260,7 +315,35 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(SPL
                 uint32_t sr;
 #define VD_PK_RN "\n\ts_nop 0\n\tv_readfirstlane_b32 %[sr], %[V]\n\ts_sub_u32 %[sr], %[sr], %[vb]\n\tv_subrev_u32 %[V], %[sr], %[V]"
 #define VD_PK_IN [fnm] "v"(FNM), [fhf] "s"(FHF), [vb] "n"(VBASE)
-                if constexpr (J == 8) {
+                if constexpr (F2) {
+                    // each chain as vd_decode_tg: bits 1..8 of the fp32 pattern into byte g of its ring word,
+                    // the field cleared; at the block end each chain renormalises by its own position 0
+                    constexpr uint32_t fnm2 = ~((1u << S) - 1u), fhf2 = 1u << (S - 1);
+                    uint32_t sr1;
+#define VD_F2_RO(SEL, UNUSED)                                                                                \
+    "v_lshrrev_b32_sdwa %[w], 1, %[V] dst_sel:" SEL " dst_unused:" UNUSED " src0_sel:DWORD src1_sel:DWORD\n\t"   \
+    "v_and_or_b32 %[V], %[V], %[fnm], %[fhf]"
+#define VD_F2_RN "\n\ts_nop 0\n\tv_readfirstlane_b32 %[sr], %[V]\n\ts_sub_u32 %[sr], %[sr], %[vb]\n\tv_subrev_u32 %[V], %[sr], %[V]"
+#define VD_F2_IN [fnm] "v"(fnm2), [fhf] "s"(fhf2), [vb] "n"(VBF)
+                    if constexpr (g == 0) {
+                        asm(VD_F2_RO("BYTE_0", "UNUSED_PAD") : [V] "+v"(V0), [w] "=&v"(wA) : VD_F2_IN);
+                        asm(VD_F2_RO("BYTE_0", "UNUSED_PAD") : [V] "+v"(V1), [w] "=&v"(wB) : VD_F2_IN);
+                    } else if constexpr (g == 1) {
+                        asm(VD_F2_RO("BYTE_1", "UNUSED_PRESERVE") : [V] "+v"(V0), [w] "+v"(wA) : VD_F2_IN);
+                        asm(VD_F2_RO("BYTE_1", "UNUSED_PRESERVE") : [V] "+v"(V1), [w] "+v"(wB) : VD_F2_IN);
+                    } else if constexpr (g == 2) {
+                        asm(VD_F2_RO("BYTE_2", "UNUSED_PRESERVE") : [V] "+v"(V0), [w] "+v"(wA) : VD_F2_IN);
+                        asm(VD_F2_RO("BYTE_2", "UNUSED_PRESERVE") : [V] "+v"(V1), [w] "+v"(wB) : VD_F2_IN);
+                    } else {
+                        asm(VD_F2_RO("BYTE_3", "UNUSED_PRESERVE") VD_F2_RN
+                            : [V] "+v"(V0), [w] "+v"(wA), [sr] "=&s"(sr) : VD_F2_IN : "scc");
+                        asm(VD_F2_RO("BYTE_3", "UNUSED_PRESERVE") VD_F2_RN
+                            : [V] "+v"(V1), [w] "+v"(wB), [sr] "=&s"(sr1) : VD_F2_IN : "scc");
+                    }
+#undef VD_F2_IN
+#undef VD_F2_RN
+#undef VD_F2_RO
+                } else if constexpr (J == 8) {
                     // bits 1..8 of each half into byte g of its ring word (SDWA)
 #define VD_PK_RO(SEL, UNUSED)                                                                                \
     "v_lshrrev_b32_sdwa %[wa], 1, %[V] dst_sel:" SEL " dst_unused:" UNUSED " src0_sel:DWORD src1_sel:DWORD\n\t"  \
@@ -309,7 +392,12 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(SPL
             wA = ~wA;
             wB = ~wB;
         }
-        if constexpr (SPL) {  // kept vectors (block ends: renormalised, fields cleared)
+        if constexpr (F2) {  // kept vectors (block ends: renormalised, fields cleared)
+            if (j == seA) kAe = __builtin_bit_cast(uint32_t, V0);
+            if (j == ssB) kBs = __builtin_bit_cast(uint32_t, V1);
+            if (j == ssA) kAs = __builtin_bit_cast(uint32_t, V0);
+            if (j == seB) kBe = __builtin_bit_cast(uint32_t, V1);
+        } else if constexpr (SPL) {  // kept vectors (block ends: renormalised, fields cleared)
             if (j == seA) sv1 = __builtin_amdgcn_perm(sv1, V, 0x07060100u);  // low half from V
             if (j == ssB) sv1 = __builtin_amdgcn_perm(V, sv1, 0x07060100u);  // high half from V
             if (j == ssA) sv2 = __builtin_amdgcn_perm(sv2, V, 0x07060100u);
@@ -364,14 +452,37 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(SPL
             lds_write_addtid4<TT::ALT_OFF + 256 * part, 8>(tabl, f(e0 + d), f(e1 + d), f(e2 + d), f(e3 + d));
         }
     };
+    // F2: each chain's row in its own table, from the two soft values (vd_decode_tg's SOFT8 form: six FMAs)
+    auto put_row_f2 = [&](auto PT, typename IN::raw_t wa, typename IN::raw_t wb) {
+        if constexpr (F2) {
+            constexpr int part = decltype(PT)::value;
+            const float tg = part ? tf0B : tf0A;
+            constexpr float SC = (float)(1 << S);
+            float s0, s1;
+            IN::s01(wa, s0, s1);
+            float X = __builtin_fmaf(s0, SC, tg), Y = __builtin_fmaf(s0, -SC, tg);
+            lds_write_addtid4<256 * part, TT::REGION>(tabl, __builtin_fmaf(s1, -SC, Y), __builtin_fmaf(s1, SC, Y),
+                                                      __builtin_fmaf(s1, -SC, X), __builtin_fmaf(s1, SC, X));
+            IN::s01(wb, s0, s1);
+            X = __builtin_fmaf(s0, SC, tg);
+            Y = __builtin_fmaf(s0, -SC, tg);
+            lds_write_addtid4<TT::BYTES + 256 * part, TT::REGION>(tabl, __builtin_fmaf(s1, -SC, Y), __builtin_fmaf(s1, SC, Y),
+                                                                  __builtin_fmaf(s1, -SC, X), __builtin_fmaf(s1, SC, X));
+        }
+    };
     const int r6a = sA % 6, r6b = sB % 6;
     using P0 = std::integral_constant<int, 0>;
     using P1 = std::integral_constant<int, 1>;
     for (uint32_t pass = 0;; pass++) {
         for (uint32_t j = 0; nblk; j += 3) {
             if constexpr (!(ABL & kAblNoTabBuild)) {
-                put_row(P0{}, rAA, rAB, sA, r6a);
-                if (lane < 32) put_row(P1{}, rBA, rBB, sB, r6b);
+                if constexpr (F2) {
+                    put_row_f2(P0{}, rAA, rAB);
+                    if (lane < 32) put_row_f2(P1{}, rBA, rBB);
+                } else {
+                    put_row(P0{}, rAA, rAB, sA, r6a);
+                    if (lane < 32) put_row(P1{}, rBA, rBB, sB, r6b);
+                }
             }
             if constexpr (LD2) {
                 rAA = nAA;
@@ -406,13 +517,13 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(SPL
         uint32_t nb = 0;
         if (tail) {
             __syncthreads();
-            wlds[LL::TAB_OFF + lane] = sv2;
+            wlds[LL::TAB_OFF + lane] = F2 ? kBe : sv2;
             __syncthreads();
             if (wv > 0) nb = lds[(wv - 1) * LL::WAVE + LL::TAB_OFF + lane];
             __syncthreads();
         }
-        const bool mA = pA > 0 && __builtin_amdgcn_ballot_w64((sv2 & 0xFFFFu) != (nb >> 16)) != 0;
-        const bool mB = __builtin_amdgcn_ballot_w64((sv1 >> 16) != (sv1 & 0xFFFFu)) != 0;
+        const bool mA = pA > 0 && __builtin_amdgcn_ballot_w64(F2 ? kAs != nb : (sv2 & 0xFFFFu) != (nb >> 16)) != 0;
+        const bool mB = __builtin_amdgcn_ballot_w64(F2 ? kBs != kAe : (sv1 >> 16) != (sv1 & 0xFFFFu)) != 0;
         const bool more = tail ? __syncthreads_or(mA || mB) != 0 : (mA || mB);
         if (!more || pass + 1u >= 2u * P) break;  // WG-uniform; after P passes no start differs
         if (lane == 0 && geo.stats && (mA || mB)) atomicAdd(geo.stats, (mA ? 1u : 0u) + (mB ? 1u : 0u));
@@ -425,8 +536,9 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(SPL
             kmaxA = pk_cut(pA + 1u, P, WA) - oA;
             ssA = ~0u;
             seA = kmaxA - 1u;
-            vA = nb >> 16;
+            vA = F2 ? nb : nb >> 16;
             sv2 = __builtin_amdgcn_perm(sv2, vA, 0x07060100u);  // its start vector
+            kAs = vA;
         }
         if (mB) {
             oB = pk_cut(pB, P, WA);
@@ -434,8 +546,9 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(SPL
             kmaxB = pk_cut(pB + 1u, P, WA) - oB;
             ssB = ~0u;
             seB = pB + 1u < P ? kmaxB - 1u : ~0u;
-            vB = sv1 & 0xFFFFu;
+            vB = F2 ? kAe : sv1 & 0xFFFFu;
             sv1 = __builtin_amdgcn_perm(vB << 16, sv1, 0x07060100u);
+            kBs = vB;
         }
         if (!mA) {  // idle A: B's job (or nothing)
             oA = oB;
@@ -450,12 +563,14 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(SPL
             vB = vA;
         }
         V = vA | vB << 16;
+        V0 = __builtin_bit_cast(float, vA);
+        V1 = __builtin_bit_cast(float, vB);
         nblk = mA || mB ? (mA ? kmaxA : kmaxB) + 2u : 0u;
         if (mA && mB && kmaxB > kmaxA) nblk = kmaxB + 2u;
         startA = stA + 32ull * oA;
         startB = stB + 32ull * oB;
         kb = 0;
-        tbn = LL::TBS - (blockIdx.x & 3u);
+        tbn = LL::TBS - (blockIdx.x & 3u) % LL::TBS;
         wave_sync();
         rsA = tg_rsrc<CH>(in, startA, availB);
         rsB = tg_rsrc<CH>(in, startB, availB);

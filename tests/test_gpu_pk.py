@@ -10,7 +10,7 @@ import numpy as np
 import pytest
 import torch
 
-from vitdec import FP32, HARD, M_B16, M_B32, M_FP16, O_B16, SOFT4
+from vitdec import FP32, HARD, M_B16, M_B32, M_FP16, O_B16, SOFT4, SOFT8
 from test_gpu_parity import name
 
 
@@ -142,3 +142,41 @@ def test_packed_split_random_input_redecodes(gpu, vo, opt):
     assert redec > 0, redec
     notail = _single(gpu, opt, packed, nin, n, {"VD_PK_TAIL": "0"})
     assert torch.equal(pk, notail)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("opt", [SOFT8 | M_B16, SOFT8 | M_B16 | O_B16], ids=name)
+@pytest.mark.parametrize("nbits,snr", [(13_107_264, 1.0), (20_000_000, 0.0), (32_000_000, 15.0)])
+def test_two_chain_soft8_split(gpu, vo, opt, nbits, snr):
+    """SOFT8 / M_B16 single-batch launches with two fp32 chains per wave (VD_F2=1, vd_kernel_pk.h F2): the
+    split layout of the packed kernels (tail workgroups included) with vd_decode_tg's fp32 tagged stage on
+    each chain; equal to the oracle and to vd_decode_tg's segment launch"""
+    n = 2 * nbits
+    packed, stride, nin = _batches(gpu, opt, nbits, snr, 1, 57)
+    f2 = _single(gpu, opt, packed, nin, n, {"VD_F2": "1"})
+    tg = _single(gpu, opt, packed, nin, n, {"VD_F2": "0"})
+    p = packed[:nin].cpu().numpy().view(np.int32)
+    ref, ok = vo.decode(opt, p, input_num=n, nthreads=16)
+    got = f2.cpu().numpy().view(ref.dtype)
+    bad = np.flatnonzero(got != ref)
+    assert bad.size == 0, f"{bad.size} of {ref.size} words differ, first {bad[:5]}"
+    assert torch.equal(f2, tg)
+
+
+@pytest.mark.gpu
+def test_two_chain_soft8_split_random_input(gpu, vo):
+    opt = SOFT8 | M_B16
+    nbits = 16_000_000
+    n = 2 * nbits
+    nin = gpu.lib().vd_input_size(opt, n)
+    g = torch.Generator(device="cpu").manual_seed(6)
+    packed = torch.randint(0, 256, (nin + 256,), dtype=torch.uint8, generator=g).to("cuda")
+    before = gpu.split_redecodes()
+    f2 = _single(gpu, opt, packed, nin, n, {"VD_F2": "1"})
+    redec = gpu.split_redecodes() - before
+    p = packed[:nin].cpu().numpy().view(np.int32)
+    ref, ok = vo.decode(opt, p, input_num=n, nthreads=16)
+    got = f2.cpu().numpy().view(ref.dtype)
+    bad = np.flatnonzero(got != ref)
+    assert bad.size == 0, f"{bad.size} of {ref.size} words differ (re-decoded: {redec}), first {bad[:5]}"
+    assert redec > 0
