@@ -142,6 +142,13 @@ launch_fn pick_pk_ch(int o)
     switch (ch_of(o)) {
     case 0: return pick_pk_ob<L + vd::HARD, SPL>(o);
     case 1: return pick_pk_ob<L + vd::SOFT4, SPL>(o);
+    // SOFT8 batched only: its split single-batch launch re-decodes nearly every chunk on noise-like input
+    // (the speculative second part rarely converges on saturated random values: 0.36 against 0.19 ms), and on
+    // codewords it measured no faster than vd_decode_tg's segment launch (0.182 against 0.181 ms)
+    case 2:
+        if constexpr (SPL) return nullptr;
+        else return out_of(o) == 1 ? (met_of(o) == 0 ? &launch_pk<L + vd::SOFT8, 0, 16, false> : &launch_pk<L + vd::SOFT8, 1, 16, false>)
+                                   : (met_of(o) == 0 ? &launch_pk<L + vd::SOFT8, 0, 32, false> : &launch_pk<L + vd::SOFT8, 1, 32, false>);
     case 4: return pick_pk_ob<L + vd::FP32, SPL>(o);
     }
     return nullptr;
@@ -151,13 +158,6 @@ launch_fn pick_pk(int o, bool llr)
 {
     return llr ? pick_pk_ch<SPL, vd::kLlr>(o) : pick_pk_ch<SPL, 0>(o);
 }
-// SOFT8 / M_B16 split launches with two fp32 chains per wave (vd_kernel_pk.h F2)
-launch_fn pick_f2(int o)
-{
-    if (ch_of(o) != 2 || met_of(o) != 1) return nullptr;
-    return out_of(o) == 1 ? &launch_pk<vd::SOFT8, 1, 16, true> : &launch_pk<vd::SOFT8, 1, 32, true>;
-}
-
 template <int L>
 launch_fn pick_ch(int o)
 {
@@ -177,7 +177,7 @@ launch_fn pick(int o, bool llr)
 }
 
 // CORE names the option's tie rule.  vd_decode_tg computes on the fp32 exact-integer tagged core (SOFT16:
-// int32 patterns); vd_decode_pk (batched HARD / SOFT4 / FP32) on exact-integer tagged int16 halves, two
+// int32 patterns); vd_decode_pk (HARD / SOFT4 / SOFT8 / FP32) on exact-integer tagged int16 halves, two
 // chunks per lane; none on fp16 arithmetic
 const char* kname(int o)
 {
@@ -194,7 +194,11 @@ const char* kname(int o)
          "vd_decode_tg<SOFT4,B16> (single batches with chunks under 64 words); M_B16 tie rule",
          "vd_decode_pk<SOFT4,F16> (int16 halves: batched, two chunks per lane; single batch, one chunk cut in two) / "
          "vd_decode_tg<SOFT4,F16> (single batches with chunks under 64 words); M_FP16 tie rule"},
-        {"vd_decode_tg<SOFT8,B32> (fp32 tagged core, M_B32 tie rule)", "vd_decode_tg<SOFT8,B16> (fp32 tagged core, M_B16 tie rule)", "-"},
+        {"vd_decode_pk<SOFT8,B32> (int16 halves, 2-stage fields: batched, two chunks per lane) / "
+         "vd_decode_tg<SOFT8,B32> (fp32 tagged core: single batches, segment launch); M_B32 tie rule",
+         "vd_decode_pk<SOFT8,B16> (int16 halves, 2-stage fields: batched, two chunks per lane) / "
+         "vd_decode_tg<SOFT8,B16> (fp32 tagged core: single batches, segment launch); M_B16 tie rule",
+         "-"},
         {"vd_decode_tg<SOFT16,B32> (int32 tagged patterns, M_B32 tie rule)", "-", "-"},
         {"vd_decode_pk<FP32,B32> (int16 halves: batched, two chunks per lane; single batch, one chunk cut in two) / "
          "vd_decode_tg<FP32,B32> (single batches with chunks under 64 words); M_B32 tie rule",
@@ -242,7 +246,6 @@ struct vd_decoder {
     int pk = 1;                 // HARD/SOFT4/FP32 launches on vd_decode_pk (VD_NO_PK=1: on vd_decode_tg)
     int pksplit = 1;            // their single-batch launches split on vd_decode_pk (VD_PK_SPLIT=0: tg segments)
     int pktail = 1;             // ... with the tail chunks in 4-wave workgroups (VD_PK_TAIL=0: one chunk per wave)
-    int f2 = 0;                 // SOFT8/M_B16 split launches with two fp32 chains per wave (VD_F2=1; study)
     uint32_t* check = nullptr;  // LDS guard violation counter (vd_set_guard_check), null = off
 };
 
@@ -367,7 +370,6 @@ static int launch_decode(const vd_decoder* d, const void* in_d, void* out_d, siz
     const bool splitok = nbatch == 1 && d->pk && d->pksplit && d->split && g.nchunks % vd::kWaves == 0 &&
                          w32 / g.nchunks >= (uint64_t)vd::kSplitMinWords;
     fp = splitok ? pick_pk<true>(options, llr) : nullptr;
-    if (!fp && splitok && !llr && d->f2) fp = pick_f2(options);
     if (fp) {
         g.stats = d->ds->stats;
         // the last nchunks mod (SIMDs) chunks one per workgroup of 4 waves (8 parts each): with 6400 chunks
@@ -442,8 +444,6 @@ int vd_create(int options, size_t preallocInputNum, int device, vd_decoder** out
     d->pksplit = pks && pks[0] == '0' ? 0 : 1;
     const char* pkt = std::getenv("VD_PK_TAIL");
     d->pktail = pkt && pkt[0] == '0' ? 0 : 1;
-    const char* f2 = std::getenv("VD_F2");
-    d->f2 = f2 && f2[0] == '1' ? 1 : 0;
     const char* chk = std::getenv("VD_CHECK");
     if (chk && chk[0] == '1') {
         int rc = vd_set_guard_check(d, 1);

@@ -1,7 +1,8 @@
-// vd_kernel_pk.h -- vd_decode_pk<CH, CORE, OB, SPL>: HARD, SOFT4 or FP32 input, two trellis chains per
+// vd_kernel_pk.h -- vd_decode_pk<CH, CORE, OB, SPL>: HARD, SOFT4, SOFT8 or FP32 input, two trellis chains per
 // wave, one in each 16-bit half of the lane's metric word: two chunks (batched launches) or two parts of one
 // chunk (SPL: single-batch split launches, below).  Same decode as vd_decode_tg<CH, CORE, OB> word for word
-// (reference viterbi_core, src/viterbi/viterbi.cu:144-207; tie rules viterbiACS.cuh:113-157,216-256).
+// (reference viterbi_core, src/viterbi/viterbi.cu:144-207; tie rules viterbiACS.cuh:113-157,216-256; the
+// int16x2 idea of selfPM/pairPM<M_B16>, viterbiACS.cuh:113-119,216-220).
 //
 // Why it is exact.  A HARD metric needs few bits: every path metric lies within D = 12 units of the best
 // one and the best grows by at most 1 unit per stage, so between two renormalisations (32 stages) the
@@ -14,8 +15,17 @@
 // word's halves ARE VA + EA and VB + EB whenever both lie in [0, 2^16) -- which the bound guarantees for
 // every sum the kernel forms (the intermediate carries of two's-complement halves cancel modulo 2^32).
 // SOFT4 / FP32 (BMmax 16, D = 192: candidates within [-209, +723] units) fit with 4-stage fields, S = 5:
-// BASE = 8192, values in [1504, 31328).  (SOFT8's spread alone, D = 3072 units, leaves no room for a
-// history field in 16 bits; it stays on vd_decode_tg.)
+// BASE = 8192, values in [1504, 31328).
+//
+// SOFT8 range (round 5).  BM = +-s0 +- s1 with s in [-128, 127]: BMmax 256, and two labels differing in one
+// output bit differ by 2|s| <= 256.  The spread of the metrics is at most 256 w, w = 11: PM[T1] - PM[T2] is at
+// most the BM difference along the two 6-stage paths into T1 and T2 from T1's survivor origin, i.e. 256 times
+// the Hamming weight of the first six output pairs of the code driven by T1 ^ T2 from the zero state, at most
+// 11 for (0171, 0133) (a chunk's first stages from equal metrics: at most 2 per stage, 10) -- D = 2816 instead
+// of (K-1)(BMmax - BMmin) = 3072.  Renormalising every R = 8 stages, the candidates of a stage lie within
+// [-D - 256, D + 8 * 256] = [-3072, 4864] units of position 0's metric: 7,937 units, so 2-stage history
+// fields (S = 3, tags -+1, -+2) fit a 16-bit half: BASE = 25600, values in [1024, 64520).
+//
 // So one v_add_u32 / v_sub_u32 adds for both chunks, v_pk_max_u16 takes both maxima, and the DPP exchange
 // rides on the subtraction (v_sub_u32_dpp: the partner's V minus the shared entry).  A DPP stage is
 // v_add_u32 + v_sub_u32_dpp + v_pk_max_u16 for two chunk-states, an LDS-exchange stage v_sub_u32 +
@@ -32,6 +42,19 @@
 // (SOFT4 / FP32): nibble g of the ring word; field pairs are gathered as c = (V >> 1) of the even field,
 // bfi(0x00F000F0, V << 3, c) of the odd one (chunk A's two fields in byte 0, chunk B's in byte 2), and at
 // the block end four v_perm_b32 turn the four pair words into the two ring words.
+// J = 2 (SOFT8): after a field F = 4 + h is odd, its take-bits d = bits 1, 2.  x = V & 0x00060006 (both
+// halves), V = (V ^ x) + 0x00030003 puts F back to 4 (one v_xad_u32; every fourth field the constant also
+// renormalises: VBASE - 0x00010001 - (V of position 0 & ~7 in each half), on the scalar unit), and
+// v_lshl_or_b32 collects d into bits 2g of two pair words (fields 0..7 and 8..15; chunk A low, chunk B high
+// half) that are the block's two ring words as they stand -- 3 VALU per field for both chunks.
+// Ring and traceback (SOFT8).  The ring is indexed by p' = rotl6(p, 1), where the two stages of a field
+// (t0 even, t0 + 1) flip position bits q' = t0 % 6 and t0 % 6 + 1 (never wrapping).  Tracing back is then
+// position arithmetic: from p' = 0 (state 0) at a block end, each field back is p' ^= d << (t0 % 6), and the
+// field's two decoded bits are bits t0 % 6, t0 % 6 + 1 of the new p' (the stored bit of an M_B32 phase-0 stage
+// in the upper position half, an own-won tag, is complemented once per block so that every stored bit is a
+// take-bit).  A lane keeps its LDS read address A = slot | 4 p' (ring slots 256-B aligned: the ring leads the
+// wave's LDS), so a step is one ds_read_u8 at a constant offset, v_bfe_u32, v_lshlrev_b32 (the lane's phase)
+// and v_xor_b32: 32 dependent steps per word (tools/pk2_model.py replays the scheme against the reference).
 #pragma once
 #include "vd_kernel_tg.h"
 
@@ -73,60 +96,64 @@ __device__ __forceinline__ void pk_stage_lds_post(uint32_t& V, uint32_t m, int p
 }
 
 // metric format per input (CH >= kLlr: float channel values quantised in the table build as for the base
-// format, vd_kernel_tg.h TgInLlr): history field length J, scale 2^S, base of a half
+// format, vd_kernel_tg.h TgInLlr): history field length J, scale 2^S, base of a half, stages between
+// renormalisations RN
 template <int CH>
 struct PkFmt {
     static constexpr int B = CH & 7;
-    // F2 (SOFT8): two fp32 chains per wave in two registers (vd_decode_tg's tagged fp32 metric each), for
-    // split single-batch launches only -- SOFT8's spread does not fit int16 halves
-    static constexpr bool F2 = B == SOFT8;
-    static constexpr int J = B == HARD || F2 ? 8 : 4;
+    static constexpr bool P2 = B == SOFT8;  // 2-stage fields, position-space ring (header)
+    static constexpr int J = B == HARD ? 8 : P2 ? 2 : 4;
     static constexpr int S = J + 1;
-    static constexpr uint32_t BASE = B == HARD ? 16384u : 8192u;
-    static_assert(B == HARD || B == SOFT4 || B == FP32 || F2, "int16 halves hold HARD, SOFT4 and FP32 metrics");
+    static constexpr uint32_t BASE = B == HARD ? 16384u : P2 ? 25600u : 8192u;
+    static constexpr int RN = P2 ? 8 : 32;
+    static_assert(B == HARD || B == SOFT4 || B == SOFT8 || B == FP32, "int16 halves hold HARD, SOFT4, SOFT8 and FP32 metrics");
 };
-// F2 stages: vd_decode_tg's tagged fp32 stage on both chains, interleaved (V0, V1 unpinned)
-template <int Q>
-__device__ __forceinline__ void f2_stage_dpp(float& V0, float& V1, float m0, float m1)
-{
-    float a0, a1, b0, b1;
-#define VD_F2_DPP(CTRL)                                                                                      \
-    asm("v_sub_f32 %4, %0, %6\n\tv_sub_f32 %5, %1, %7\n\tv_add_f32 %2, %0, %6\n\tv_add_f32 %3, %1, %7\n\t"       \
-        "v_max_f32_dpp %0, %4, %2 " CTRL " row_mask:0xf bank_mask:0xf\n\t"                                      \
-        "v_max_f32_dpp %1, %5, %3 " CTRL " row_mask:0xf bank_mask:0xf"                                          \
-        : "+v"(V0), "+v"(V1), "=&v"(a0), "=&v"(a1), "=&v"(b0), "=&v"(b1) : "v"(m0), "v"(m1))
-    if constexpr (Q == 0) VD_F2_DPP("quad_perm:[1,0,3,2]");
-    else if constexpr (Q == 1) VD_F2_DPP("quad_perm:[2,3,0,1]");
-    else if constexpr (Q == 2) VD_F2_DPP("row_half_mirror");
-    else VD_F2_DPP("row_ror:8");
-#undef VD_F2_DPP
-}
-template <bool X32>
-__device__ __forceinline__ void f2_stage_lds_pre(float& V0, float& V1, float m0, float m1, int paddr)
-{
-    float a0, a1, b0, b1;
-    asm("v_sub_f32 %0, %2, %3\n\tv_sub_f32 %1, %4, %5" : "=&v"(b0), "=&v"(b1) : "v"(V0), "v"(m0), "v"(V1), "v"(m1));
-    const float p0 = X32 ? tg_partner(b0, paddr) : tg_swz16(b0);
-    const float p1 = X32 ? tg_partner(b1, paddr) : tg_swz16(b1);
-    asm("v_add_f32 %0, %2, %3\n\tv_add_f32 %1, %4, %5" : "=&v"(a0), "=&v"(a1) : "v"(V0), "v"(m0), "v"(V1), "v"(m1));
-    asm("v_max_f32 %0, %1, %2" : "=v"(V0) : "v"(a0), "v"(p0));
-    asm("v_max_f32 %0, %1, %2" : "=v"(V1) : "v"(a1), "v"(p1));
-}
 
-// LDS layout of a wave (words), for NW resident workgroups (waves per SIMD) per CU
-template <int NW = 8, bool F2 = false>
+// LDS layout of a wave (words), for NW resident workgroups (waves per SIMD) per CU.  P2 (SOFT8): the ring
+// leads (its slots are 256-B aligned for the XOR addressing of the traceback): [ring | guard | table | guard |
+// guard], a slot = two words per position (fields 0..7 and 8..15; chunk A in the low, chunk B in the high half)
+template <int NW = 8, bool P2 = false>
 struct PkLds {
     static constexpr int GW = kGuardWords;
-    static constexpr int TAB = F2 ? 2 * TgTabL::BYTES / 4 : TgTabLT<true>::BYTES / 4;  // F2: a table per chain
+    static constexpr int TAB = TgTabLT<true>::BYTES / 4;
     static constexpr int LDSW = 163840 / 4 / (NW * kWaves);                // a wave's share
     static constexpr int TBS = (LDSW - 3 * GW - TAB) / 128 - 1;            // words per traceback batch and chunk
     static constexpr int RING = (TBS + 1) * 64;                            // words per chunk ring
-    static constexpr int TAB_OFF = GW, RING_OFF = 2 * GW + TAB;
-    static constexpr int WAVE = 3 * GW + TAB + 2 * RING;
-    static __device__ __forceinline__ int guard(int i) { return i < GW ? i : i < 2 * GW ? TAB + i : TAB + 2 * RING + i; }
+    static constexpr int TAB_OFF = P2 ? 2 * RING + GW : GW, RING_OFF = P2 ? 0 : 2 * GW + TAB;
+    static constexpr int WAVE0 = 3 * GW + TAB + 2 * RING;
+    static constexpr int WAVE = P2 ? (WAVE0 + 63) / 64 * 64 : WAVE0;
+    static __device__ __forceinline__ int guard(int i)
+    {
+        if constexpr (P2) return 2 * RING + (i < GW ? i : TAB + i);
+        return i < GW ? i : i < 2 * GW ? TAB + i : TAB + 2 * RING + i;
+    }
 };
 static_assert(PkLds<8>::TBS == 5 && kWaves * PkLds<8>::WAVE * 4 <= 20480, "8 workgroups of 4 waves per CU");
-static_assert(PkLds<7, true>::TBS == 3 && kWaves * PkLds<7, true>::WAVE * 4 <= 163840 / 7, "F2: 7 workgroups per CU");
+static_assert(PkLds<8, true>::TBS == 5 && kWaves * PkLds<8, true>::WAVE * 4 <= 20480 && PkLds<8, true>::WAVE % 64 == 0,
+              "SOFT8: 8 workgroups of 4 waves per CU, ring slots 256-B aligned");
+
+// SOFT8 traceback of one word (header "Ring and traceback"): A = the lane's emit slot (block k + 1; the
+// convergence block k + 2 is the next slot, +512 B) | 2 for chunk B's half; z[r] = 2 + the position bit of the
+// first stage of convergence-block field g (g % 3 = r); the emit block's field g has z[(g + 2) % 3].
+template <int CORE>
+__device__ __forceinline__ uint32_t pk2_traceback(uint32_t A, const uint32_t (&z)[3])
+{
+    typedef const __attribute__((address_space(3))) uint8_t* lp8;
+    uint32_t nat = 0;
+    auto step = [&](auto EMc, auto Gc) {
+        constexpr bool EM = decltype(EMc)::value;
+        constexpr int g = decltype(Gc)::value;
+        constexpr int off = (EM ? 0 : 512) + 256 * (g / 8) + (g % 8) / 4;
+        const uint32_t B = ((lp8)(uintptr_t)A)[off];
+        const uint32_t d = __builtin_amdgcn_ubfe(B, 2 * (g % 4), 2);
+        const uint32_t zz = z[EM ? (g + 2) % 3 : g % 3];
+        A ^= d << zz;
+        if constexpr (EM) nat |= __builtin_amdgcn_ubfe(A, zz, 2) << (2 * g);  // bit s <-> block stage s
+    };
+    sfor<16>([&](auto I) { step(std::false_type{}, std::integral_constant<int, 15 - decltype(I)::value>{}); });
+    sfor<16>([&](auto I) { step(std::true_type{}, std::integral_constant<int, 15 - decltype(I)::value>{}); });
+    return __builtin_bitreverse32(nat);  // word bit i <-> stage 63+32k-i
+}
 
 // Split single-batch launches (SPL).  A chunk of W words is cut into P parts at words cut(1) .. cut(P-1),
 // multiples of 3 blocks; part p emits words [cut(p), cut(p+1)).  Part 0 decodes from the chunk start (equal
@@ -151,20 +178,20 @@ __host__ __device__ constexpr uint32_t pk_cut(uint32_t p, uint32_t P, uint32_t W
 }
 
 // NW, ABL: tools only (waves per SIMD of the LDS layout; component ablations as vd_decode_tg's, wrong outputs)
-template <int CH, int CORE, int OB = 32, bool SPL = false, int NW = (PkFmt<CH>::F2 ? 7 : 8), int ABL = 0>
+template <int CH, int CORE, int OB = 32, bool SPL = false, int NW = 8, int ABL = 0>
 __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(SPL ? 7 : NW))) void vd_decode_pk(const void* __restrict__ in_all, void* __restrict__ out_all, Geom geo)
 {
-    constexpr bool F2 = PkFmt<CH>::F2;
-    static_assert(!F2 || (SPL && CORE == B16 && NW == 7), "F2: split launches of the M_B16 core");
+    constexpr bool P2 = PkFmt<CH>::P2;
     using IN = TgIn<CH>;
-    using TT = std::conditional_t<F2, TgTabL, TgTabLT<true>>;
-    using LL = PkLds<NW, F2>;
+    using TT = TgTabLT<true>;
+    using LL = PkLds<NW, P2>;
     constexpr int J = PkFmt<CH>::J, S = PkFmt<CH>::S;
-    constexpr bool ALT = CORE == B32 && !F2;  // M_B32: the upper position half takes the +tag entries at phase 0
-    __shared__ __attribute__((aligned(16))) uint32_t lds[kWaves * LL::WAVE];
+    constexpr bool ALT = CORE == B32;  // M_B32: the upper position half takes the +tag entries at phase 0
+    __shared__ __attribute__((aligned(256))) uint32_t lds[kWaves * LL::WAVE];
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int pos = tg_pos(lane);
+    const int pp = ((pos << 1) | (pos >> 5)) & 63;  // P2: ring index p' = rotl6(p, 1)
     uint32_t* const wlds = lds + wv * LL::WAVE;
     char* const tabb = (char*)(wlds + LL::TAB_OFF);
     uint32_t* const ringA = wlds + LL::RING_OFF;
@@ -191,13 +218,14 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(SPL
         aK[K] = LSTR * own_label(pos, K);
     });
     if constexpr (ALT) aK[0] = upper5 ? TT::ALT_OFF + 8 * own_label(pos, 0) : aK[0];
+    // P2, M_B32: the upper position half's phase-0 bits are own-won tags; complemented at the block end
+    const uint32_t up5m = upper5 ? ~0u : 0u;
     const int pa5 = 4 * (lane ^ 32);
     // table-build roles (as vd_decode_tg): lane l builds table index l (stage sA), lanes 0..31 also 64 + l (sB)
     const int sA = TgTabL::stage(lane), sB = TgTabL::stage(64 + (lane & 31));
     const int tagA = 1 << (sA % J), tagB = 1 << (sB % J);
     // entry tag of the row's own class, both halves: tg0 * 65537 (M_FP16: own wins ties, +2^j; else -2^j)
     const int32_t tg0A = (CORE == F16 ? tagA : -tagA) * 65537, tg0B = (CORE == F16 ? tagB : -tagB) * 65537;
-    const float tf0A = -(float)tagA, tf0B = -(float)tagB;  // F2 (M_B16: exchanged wins ties)
     const uint32_t tabl = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)tabb;
     constexpr uint32_t BASE = PkFmt<CH>::BASE;
     constexpr uint32_t VB1 = BASE + (1u << (S - 1));  // a half with metric 0 and a cleared field
@@ -233,12 +261,6 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(SPL
     uint64_t startA = stA + 32ull * oA, startB = stB + 32ull * oB;
     uint32_t nblk = (kmaxA > kmaxB ? kmaxA : kmaxB) + 2;
     uint32_t V = VBASE;
-    // F2: the chains' fp32 metrics (vd_decode_tg: V in [2^23, 2^24), base 1.25 2^23 + 2^(S-1)) and their kept
-    // vectors (bit patterns: A's start / end, B's start / end)
-    constexpr uint32_t VBF = 0x4B200000u + (1u << (S - 1));
-    float V0 = __builtin_bit_cast(float, VBF), V1 = V0;
-    uint32_t kAs = 0, kAe = 0, kBs = 0, kBe = 0;
-    (void)V0, (void)V1, (void)kAs, (void)kAe, (void)kBs, (void)kBe;
     // SPL: kept vectors, one per half: sv1 = (A's end, B's start), sv2 = (A's start, B's end) (low, high)
     uint32_t sv1 = 0, sv2 = 0;
     uint32_t kb = 0;
@@ -263,31 +285,25 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(SPL
     const char* const tbring = (const char*)(tbB ? ringB : ringA);
     const uint64_t tbStart = tbB ? crB.startWord : crA.startWord;
     const uint32_t tbWords = tbB ? crB.words : crA.words;
+    // P2: the lane's emit-slot LDS address without the slot index (chunk B: the high half of each word)
+    const uint32_t tbA2 = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)(const char*)ringA +
+                          512u * tbl + (tbB ? 2u : 0u);
 
     typedef uint32_t u2v __attribute__((ext_vector_type(2)));
     typedef __attribute__((address_space(3))) const volatile u2v* lptr;
     const __attribute__((address_space(3))) char* tl = (const __attribute__((address_space(3))) char*)tabb;
-    constexpr int TGD = F2 ? 2 : 4;  // table reads ahead (F2: two tables, registers for 2)
+    constexpr int TGD = 4;  // table reads ahead
     u2v vp[96];
-    typedef __attribute__((address_space(3))) const volatile f2v* lptrf;
-    f2v vf0[96], vf1[96];  // F2: the chains' entry pairs (two tables)
     auto issue = [&](auto Rc) {
         constexpr int r = decltype(Rc)::value;
         constexpr int K = r % 6;
-        if constexpr (F2) {
-            if constexpr ((r / 6) % 2 == 0) {
-                vf0[r] = *(lptrf)(tl + aK[K] + TT::row(r));
-                vf1[r] = *(lptrf)(tl + TT::BYTES + aK[K] + TT::row(r));
-            }
-        } else if constexpr ((r / 6) % 2 == 0 && !(ABL & kAblNoTabReads)) {
-            vp[r] = *(lptr)(tl + aK[K] + TT::row(r));
-        }
+        if constexpr ((r / 6) % 2 == 0 && !(ABL & kAblNoTabReads)) vp[r] = *(lptr)(tl + aK[K] + TT::row(r));
     };
     auto block = [&](auto PHc, uint32_t j) {
         constexpr int PH = decltype(PHc)::value;
         constexpr int BB = PH / 2;
         uint32_t wA = 0, wB = 0;
-        uint32_t cw[4];  // J = 4: field-pair words
+        uint32_t cw[4];  // J = 4: field-pair words; J = 2: the two ring words
         (void)cw;
         sfor<32>([&](auto I) {
             constexpr int i = decltype(I)::value;
@@ -296,53 +312,34 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(SPL
             constexpr int r = 32 * BB + i;
             constexpr bool ODD = (r / 6) % 2 == 1;
             constexpr int RP = ODD ? r - 6 : r;
-            if constexpr (F2) {
-                const float m0 = ODD ? vf0[RP].y : vf0[RP].x, m1 = ODD ? vf1[RP].y : vf1[RP].x;
-                if constexpr (Q <= 3) f2_stage_dpp<Q>(V0, V1, m0, m1);
-                else f2_stage_lds_pre<Q == 5>(V0, V1, m0, m1, pa5);
-            } else {
             const uint32_t m = (ABL & kAblNoTabReads) ? (uint32_t)aK[K] : ODD ? vp[RP].y : vp[RP].x;
             if constexpr (Q <= 3) pk_stage_dpp<Q>(V, m);
             else if constexpr (Q == 4) pk_stage_lds_pre<false>(V, m, pa5);
             else if constexpr (ALT) pk_stage_lds_post(V, m, pa5);
             else pk_stage_lds_pre<true>(V, m, pa5);
-            }
             if constexpr (r + TGD < 96) issue(std::integral_constant<int, r + TGD>{});
             if constexpr (i % J == J - 1 && !(ABL & kAblNoReadout)) {
-                // field read-out, both chunks, then both fields cleared; at the block end the renormalisation
-                // on the whole word (vd_decode_tg)
+                // field read-out, both chunks, then both fields cleared; renormalisation on the whole word
+                // (vd_decode_tg) every RN stages
                 constexpr int g = (i % 32) / J;
                 uint32_t sr;
 #define VD_PK_RN "\n\ts_nop 0\n\tv_readfirstlane_b32 %[sr], %[V]\n\ts_sub_u32 %[sr], %[sr], %[vb]\n\tv_subrev_u32 %[V], %[sr], %[V]"
 #define VD_PK_IN [fnm] "v"(FNM), [fhf] "s"(FHF), [vb] "n"(VBASE)
-                if constexpr (F2) {
-                    // each chain as vd_decode_tg: bits 1..8 of the fp32 pattern into byte g of its ring word,
-                    // the field cleared; at the block end each chain renormalises by its own position 0
-                    constexpr uint32_t fnm2 = ~((1u << S) - 1u), fhf2 = 1u << (S - 1);
-                    uint32_t sr1;
-#define VD_F2_RO(SEL, UNUSED)                                                                                \
-    "v_lshrrev_b32_sdwa %[w], 1, %[V] dst_sel:" SEL " dst_unused:" UNUSED " src0_sel:DWORD src1_sel:DWORD\n\t"   \
-    "v_and_or_b32 %[V], %[V], %[fnm], %[fhf]"
-#define VD_F2_RN "\n\ts_nop 0\n\tv_readfirstlane_b32 %[sr], %[V]\n\ts_sub_u32 %[sr], %[sr], %[vb]\n\tv_subrev_u32 %[V], %[sr], %[V]"
-#define VD_F2_IN [fnm] "v"(fnm2), [fhf] "s"(fhf2), [vb] "n"(VBF)
-                    if constexpr (g == 0) {
-                        asm(VD_F2_RO("BYTE_0", "UNUSED_PAD") : [V] "+v"(V0), [w] "=&v"(wA) : VD_F2_IN);
-                        asm(VD_F2_RO("BYTE_0", "UNUSED_PAD") : [V] "+v"(V1), [w] "=&v"(wB) : VD_F2_IN);
-                    } else if constexpr (g == 1) {
-                        asm(VD_F2_RO("BYTE_1", "UNUSED_PRESERVE") : [V] "+v"(V0), [w] "+v"(wA) : VD_F2_IN);
-                        asm(VD_F2_RO("BYTE_1", "UNUSED_PRESERVE") : [V] "+v"(V1), [w] "+v"(wB) : VD_F2_IN);
-                    } else if constexpr (g == 2) {
-                        asm(VD_F2_RO("BYTE_2", "UNUSED_PRESERVE") : [V] "+v"(V0), [w] "+v"(wA) : VD_F2_IN);
-                        asm(VD_F2_RO("BYTE_2", "UNUSED_PRESERVE") : [V] "+v"(V1), [w] "+v"(wB) : VD_F2_IN);
-                    } else {
-                        asm(VD_F2_RO("BYTE_3", "UNUSED_PRESERVE") VD_F2_RN
-                            : [V] "+v"(V0), [w] "+v"(wA), [sr] "=&s"(sr) : VD_F2_IN : "scc");
-                        asm(VD_F2_RO("BYTE_3", "UNUSED_PRESERVE") VD_F2_RN
-                            : [V] "+v"(V1), [w] "+v"(wB), [sr] "=&s"(sr1) : VD_F2_IN : "scc");
-                    }
-#undef VD_F2_IN
-#undef VD_F2_RN
-#undef VD_F2_RO
+                if constexpr (J == 2) {
+                    // x = both take-bit pairs; V = (V ^ x) + 0x00030003 (F odd: back to 4), every fourth field
+                    // + the renormalisation, VBASE - 0x00010001 - (position 0's V & ~7 per half) (header)
+                    constexpr int h = g % 8;
+                    uint32_t x;
+                    if constexpr (i % PkFmt<CH>::RN == PkFmt<CH>::RN - 1)
+                        asm("v_and_b32 %[x], 0x60006, %[V]\n\ts_nop 0\n\tv_readfirstlane_b32 %[sr], %[V]\n\t"
+                            "s_and_b32 %[sr], %[sr], 0xfff8fff8\n\ts_sub_u32 %[sr], %[vb], %[sr]\n\t"
+                            "v_xad_u32 %[V], %[V], %[x], %[sr]"
+                            : [V] "+{v60}"(V), [x] "=&v"(x), [sr] "=&s"(sr) : [vb] "n"(VBASE - 0x10001u) : "scc");
+                    else
+                        asm("v_and_b32 %[x], 0x60006, %[V]\n\tv_xad_u32 %[V], %[V], %[x], %[c]"
+                            : [V] "+{v60}"(V), [x] "=&v"(x) : [c] "s"(0x30003u));
+                    if constexpr (h == 0) cw[g / 8] = x >> 1;
+                    else cw[g / 8] = (x << (2 * h - 1)) | cw[g / 8];
                 } else if constexpr (J == 8) {
                     // bits 1..8 of each half into byte g of its ring word (SDWA)
 #define VD_PK_RO(SEL, UNUSED)                                                                                \
@@ -388,16 +385,23 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(SPL
             wA = __builtin_amdgcn_perm(p23, p01, 0x05040100u);
             wB = __builtin_amdgcn_perm(p23, p01, 0x07060302u);
         }
+        if constexpr (J == 2) {
+            // the ring words are cw[0], cw[1]; M_B32: complement the upper half's phase-0 bits (fields g with
+            // (PH + 2g) % 6 == 0: bit 0 of their pair, both chunks)
+            if constexpr (ALT) {
+                constexpr uint32_t F0 = (PH == 0 ? 0x1041u : PH == 2 ? 0x0410u : 0x4104u) * 65537u;  // g 0..7
+                constexpr uint32_t F1 = (PH == 0 ? 0x4104u : PH == 2 ? 0x1041u : 0x0410u) * 65537u;  // g 8..15
+                cw[0] ^= up5m & F0;
+                cw[1] ^= up5m & F1;
+            }
+            wA = cw[0];
+            wB = cw[1];
+        }
         if constexpr (CORE == F16) {
             wA = ~wA;
             wB = ~wB;
         }
-        if constexpr (F2) {  // kept vectors (block ends: renormalised, fields cleared)
-            if (j == seA) kAe = __builtin_bit_cast(uint32_t, V0);
-            if (j == ssB) kBs = __builtin_bit_cast(uint32_t, V1);
-            if (j == ssA) kAs = __builtin_bit_cast(uint32_t, V0);
-            if (j == seB) kBe = __builtin_bit_cast(uint32_t, V1);
-        } else if constexpr (SPL) {  // kept vectors (block ends: renormalised, fields cleared)
+        if constexpr (SPL) {  // kept vectors (block ends: renormalised, fields cleared)
             if (j == seA) sv1 = __builtin_amdgcn_perm(sv1, V, 0x07060100u);  // low half from V
             if (j == ssB) sv1 = __builtin_amdgcn_perm(V, sv1, 0x07060100u);  // high half from V
             if (j == ssA) sv2 = __builtin_amdgcn_perm(sv2, V, 0x07060100u);
@@ -405,16 +409,30 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(SPL
         }
         wave_sync();
         if (j >= 1) {
-            ringA[(j - 1 - kb) * 64 + pos] = wA;
-            ringB[(j - 1 - kb) * 64 + pos] = wB;
+            if constexpr (P2) {
+                ringA[(j - 1 - kb) * 128 + pp] = wA;
+                ringA[(j - 1 - kb) * 128 + 64 + pp] = wB;
+            } else {
+                ringA[(j - 1 - kb) * 64 + pos] = wA;
+                ringB[(j - 1 - kb) * 64 + pos] = wB;
+            }
         }
         if (j >= 2 && (j - 1 - kb == tbn || j == nblk - 1)) {
             wave_sync();
             const uint32_t nw = j - 1 - kb;
             const uint32_t k = kb + tbl;
             if (!(ABL & kAblNoTraceback) && tbl < nw && k >= (tbB ? kminB : kminA) && k < (tbB ? kmaxB : kmaxA)) {
-                const TbC tc = tb_direct<(J < 6 ? 6 : J), CORE == B32>((int)k);
-                const uint32_t w = traceback_word_tg<J, CORE == B32>(tbring, (tbl + 1u) * 256u, tc);
+                uint32_t w;
+                if constexpr (P2) {
+                    // the stage phase of the convergence block k + 2: field g of it starts at position bit
+                    // 2 ((k + 2 + g) % 3)
+                    const uint32_t u = (k + 2u) % 3u;
+                    const uint32_t z[3] = {2u * u + 2u, u == 2u ? 2u : 2u * u + 4u, u == 0u ? 6u : 2u * u};
+                    w = pk2_traceback<CORE>(tbA2, z);
+                } else {
+                    const TbC tc = tb_direct<(J < 6 ? 6 : J), CORE == B32>((int)k);
+                    w = traceback_word_tg<J, CORE == B32>(tbring, (tbl + 1u) * 256u, tc);
+                }
                 const uint32_t kc = k + (tbB ? oB : oA);  // chunk word
                 if constexpr (ABL & kAblNoStores) {
                     sink ^= w + kc;
@@ -427,15 +445,21 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(SPL
                 }
             }
             wave_sync();
-            ringA[pos] = wA;  // block j becomes slot 0 of the next batch
-            ringB[pos] = wB;
+            if constexpr (P2) {  // block j becomes slot 0 of the next batch
+                ringA[pp] = wA;
+                ringA[64 + pp] = wB;
+            } else {
+                ringA[pos] = wA;
+                ringB[pos] = wB;
+            }
             kb = j - 1;
             tbn = LL::TBS;
         }
         return j + 1 < nblk;
     };
     // the four entries of a stage for both chunks: E[L] = BM[L] * 2^S + tg0 per half (TgFmt::INT's table),
-    // from (A, B) = (BM[3], BM[2]) of each chunk packed as A_A + A_B * 2^16 (signed halves, |.| <= 16: an i24)
+    // from (A, B) = (BM[3], BM[2]) of each chunk packed as A_A + A_B * 2^16 (signed halves; |.| <= 16 except
+    // SOFT8's 256: its entries by shifts, since BM_B * 2^16 leaves __mul24's 24 bits)
     auto put_row = [&](auto PT, typename IN::raw_t wa, typename IN::raw_t wb, int li, int K) {
         constexpr int part = decltype(PT)::value;
         const int32_t tg = part ? tg0B : tg0A;
@@ -444,30 +468,22 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(SPL
         IN::ab(wb, li, AB, BBv, geo.scale);
         const int32_t pa = AA + AB * 65536, pb = BA + BBv * 65536;
         auto f = [](int32_t x) { return __builtin_bit_cast(float, x); };
-        const int32_t e3 = __mul24(pa, 1 << S) + tg, e2 = __mul24(pb, 1 << S) + tg;
-        const int32_t e0 = __mul24(pa, -(1 << S)) + tg, e1 = __mul24(pb, -(1 << S)) + tg;
+        int32_t e0, e1, e2, e3;
+        if constexpr (P2) {
+            e3 = (int32_t)((uint32_t)pa << S) + tg;
+            e2 = (int32_t)((uint32_t)pb << S) + tg;
+            e0 = 2 * tg - e3;
+            e1 = 2 * tg - e2;
+        } else {
+            e3 = __mul24(pa, 1 << S) + tg;
+            e2 = __mul24(pb, 1 << S) + tg;
+            e0 = __mul24(pa, -(1 << S)) + tg;
+            e1 = __mul24(pb, -(1 << S)) + tg;
+        }
         lds_write_addtid4<256 * part, TT::REGION>(tabl, f(e0), f(e1), f(e2), f(e3));
         if (ALT && K == 0) {  // phase-0 lanes: the +tag entries E+[L] = BM[L] * 2^S - tg0 (ALT area)
             const int32_t d = -2 * tg;
             lds_write_addtid4<TT::ALT_OFF + 256 * part, 8>(tabl, f(e0 + d), f(e1 + d), f(e2 + d), f(e3 + d));
-        }
-    };
-    // F2: each chain's row in its own table, from the two soft values (vd_decode_tg's SOFT8 form: six FMAs)
-    auto put_row_f2 = [&](auto PT, typename IN::raw_t wa, typename IN::raw_t wb) {
-        if constexpr (F2) {
-            constexpr int part = decltype(PT)::value;
-            const float tg = part ? tf0B : tf0A;
-            constexpr float SC = (float)(1 << S);
-            float s0, s1;
-            IN::s01(wa, s0, s1);
-            float X = __builtin_fmaf(s0, SC, tg), Y = __builtin_fmaf(s0, -SC, tg);
-            lds_write_addtid4<256 * part, TT::REGION>(tabl, __builtin_fmaf(s1, -SC, Y), __builtin_fmaf(s1, SC, Y),
-                                                      __builtin_fmaf(s1, -SC, X), __builtin_fmaf(s1, SC, X));
-            IN::s01(wb, s0, s1);
-            X = __builtin_fmaf(s0, SC, tg);
-            Y = __builtin_fmaf(s0, -SC, tg);
-            lds_write_addtid4<TT::BYTES + 256 * part, TT::REGION>(tabl, __builtin_fmaf(s1, -SC, Y), __builtin_fmaf(s1, SC, Y),
-                                                                  __builtin_fmaf(s1, -SC, X), __builtin_fmaf(s1, SC, X));
         }
     };
     const int r6a = sA % 6, r6b = sB % 6;
@@ -476,13 +492,8 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(SPL
     for (uint32_t pass = 0;; pass++) {
         for (uint32_t j = 0; nblk; j += 3) {
             if constexpr (!(ABL & kAblNoTabBuild)) {
-                if constexpr (F2) {
-                    put_row_f2(P0{}, rAA, rAB);
-                    if (lane < 32) put_row_f2(P1{}, rBA, rBB);
-                } else {
-                    put_row(P0{}, rAA, rAB, sA, r6a);
-                    if (lane < 32) put_row(P1{}, rBA, rBB, sB, r6b);
-                }
+                put_row(P0{}, rAA, rAB, sA, r6a);
+                if (lane < 32) put_row(P1{}, rBA, rBB, sB, r6b);
             }
             if constexpr (LD2) {
                 rAA = nAA;
@@ -517,13 +528,13 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(SPL
         uint32_t nb = 0;
         if (tail) {
             __syncthreads();
-            wlds[LL::TAB_OFF + lane] = F2 ? kBe : sv2;
+            wlds[LL::TAB_OFF + lane] = sv2;
             __syncthreads();
             if (wv > 0) nb = lds[(wv - 1) * LL::WAVE + LL::TAB_OFF + lane];
             __syncthreads();
         }
-        const bool mA = pA > 0 && __builtin_amdgcn_ballot_w64(F2 ? kAs != nb : (sv2 & 0xFFFFu) != (nb >> 16)) != 0;
-        const bool mB = __builtin_amdgcn_ballot_w64(F2 ? kBs != kAe : (sv1 >> 16) != (sv1 & 0xFFFFu)) != 0;
+        const bool mA = pA > 0 && __builtin_amdgcn_ballot_w64((sv2 & 0xFFFFu) != (nb >> 16)) != 0;
+        const bool mB = __builtin_amdgcn_ballot_w64((sv1 >> 16) != (sv1 & 0xFFFFu)) != 0;
         const bool more = tail ? __syncthreads_or(mA || mB) != 0 : (mA || mB);
         if (!more || pass + 1u >= 2u * P) break;  // WG-uniform; after P passes no start differs
         if (lane == 0 && geo.stats && (mA || mB)) atomicAdd(geo.stats, (mA ? 1u : 0u) + (mB ? 1u : 0u));
@@ -536,9 +547,8 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(SPL
             kmaxA = pk_cut(pA + 1u, P, WA) - oA;
             ssA = ~0u;
             seA = kmaxA - 1u;
-            vA = F2 ? nb : nb >> 16;
+            vA = nb >> 16;
             sv2 = __builtin_amdgcn_perm(sv2, vA, 0x07060100u);  // its start vector
-            kAs = vA;
         }
         if (mB) {
             oB = pk_cut(pB, P, WA);
@@ -546,9 +556,8 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(SPL
             kmaxB = pk_cut(pB + 1u, P, WA) - oB;
             ssB = ~0u;
             seB = pB + 1u < P ? kmaxB - 1u : ~0u;
-            vB = F2 ? kAe : sv1 & 0xFFFFu;
+            vB = sv1 & 0xFFFFu;
             sv1 = __builtin_amdgcn_perm(vB << 16, sv1, 0x07060100u);
-            kBs = vB;
         }
         if (!mA) {  // idle A: B's job (or nothing)
             oA = oB;
@@ -563,8 +572,6 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(SPL
             vB = vA;
         }
         V = vA | vB << 16;
-        V0 = __builtin_bit_cast(float, vA);
-        V1 = __builtin_bit_cast(float, vB);
         nblk = mA || mB ? (mA ? kmaxA : kmaxB) + 2u : 0u;
         if (mA && mB && kmaxB > kmaxA) nblk = kmaxB + 2u;
         startA = stA + 32ull * oA;

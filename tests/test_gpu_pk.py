@@ -1,6 +1,6 @@
-"""Batched HARD, SOFT4 and FP32 launches on vd_decode_pk (vd_kernel_pk.h): two chunks per wave, one in each
-16-bit half of the metric word (HARD: 8-stage history fields; SOFT4 / FP32: 4-stage fields), 32- and 16-bit
-output words.  Every batch must equal the oracle word for word and the fp32 tagged kernel's output
+"""Batched HARD, SOFT4, SOFT8 and FP32 launches on vd_decode_pk (vd_kernel_pk.h): two chunks per wave, one in
+each 16-bit half of the metric word (HARD: 8-stage history fields; SOFT4 / FP32: 4-stage fields; SOFT8:
+2-stage fields, renormalised every 8 stages, position-space ring and traceback), 32- and 16-bit output words.  Every batch must equal the oracle word for word and the fp32 tagged kernel's output
 (VD_NO_PK=1 at decoder creation selects it), for every metric core's tie rule, including chunk counts where
 the two chunks of a wave differ in length (an odd number of long chunks), partitions with empty chunks, and
 saturated inputs (SNR 15: the best path gains every stage, the largest range the int16 halves must hold)."""
@@ -46,7 +46,8 @@ def _decode_batched(gpu, opt, packed, stride, n, nb, no_pk):
     return out, ostride, nout
 
 
-PK_OPTS = [ch | me for ch in (HARD, SOFT4, FP32) for me in (M_B32, M_B16, M_FP16)] + [HARD | M_B32 | O_B16, FP32 | M_FP16 | O_B16]
+PK_OPTS = ([ch | me for ch in (HARD, SOFT4, FP32) for me in (M_B32, M_B16, M_FP16)] + [SOFT8 | M_B32, SOFT8 | M_B16] +
+           [HARD | M_B32 | O_B16, FP32 | M_FP16 | O_B16, SOFT8 | M_B16 | O_B16, SOFT8 | M_B32 | O_B16])
 
 
 def test_packed_kernel_names():
@@ -144,39 +145,45 @@ def test_packed_split_random_input_redecodes(gpu, vo, opt):
     assert torch.equal(pk, notail)
 
 
-@pytest.mark.gpu
-@pytest.mark.parametrize("opt", [SOFT8 | M_B16, SOFT8 | M_B16 | O_B16], ids=name)
-@pytest.mark.parametrize("nbits,snr", [(13_107_264, 1.0), (20_000_000, 0.0), (32_000_000, 15.0)])
-def test_two_chain_soft8_split(gpu, vo, opt, nbits, snr):
-    """SOFT8 / M_B16 single-batch launches with two fp32 chains per wave (VD_F2=1, vd_kernel_pk.h F2): the
-    split layout of the packed kernels (tail workgroups included) with vd_decode_tg's fp32 tagged stage on
-    each chain; equal to the oracle and to vd_decode_tg's segment launch"""
-    n = 2 * nbits
-    packed, stride, nin = _batches(gpu, opt, nbits, snr, 1, 57)
-    f2 = _single(gpu, opt, packed, nin, n, {"VD_F2": "1"})
-    tg = _single(gpu, opt, packed, nin, n, {"VD_F2": "0"})
-    p = packed[:nin].cpu().numpy().view(np.int32)
-    ref, ok = vo.decode(opt, p, input_num=n, nthreads=16)
-    got = f2.cpu().numpy().view(ref.dtype)
-    bad = np.flatnonzero(got != ref)
-    assert bad.size == 0, f"{bad.size} of {ref.size} words differ, first {bad[:5]}"
-    assert torch.equal(f2, tg)
+def _soft8_pattern(kind, nin, seed):
+    """SOFT8 channel bytes that stress the int16 range of the 2-stage-field format: every byte -128 (BM +-256
+    every stage), every byte 127, saturated random signs (-128 / 127), and uniformly random bytes"""
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    if kind == "all_min":
+        return torch.full((nin,), 0x80, dtype=torch.uint8)
+    if kind == "all_max":
+        return torch.full((nin,), 0x7F, dtype=torch.uint8)
+    if kind == "saturated":
+        return torch.where(torch.randint(0, 2, (nin,), generator=g) == 1, 0x7F, 0x80).to(torch.uint8)
+    return torch.randint(0, 256, (nin,), dtype=torch.uint8, generator=g)
 
 
 @pytest.mark.gpu
-def test_two_chain_soft8_split_random_input(gpu, vo):
-    opt = SOFT8 | M_B16
-    nbits = 16_000_000
+@pytest.mark.parametrize("opt", [SOFT8 | M_B16, SOFT8 | M_B32], ids=name)
+@pytest.mark.parametrize("kind", ["all_min", "all_max", "saturated", "random"])
+def test_packed_soft8_extreme_inputs(gpu, vo, opt, kind):
+    """SOFT8 on vd_decode_pk: batched launches (3 batches) of synthetic channel bytes at the ends of the metric
+    range (header of vd_kernel_pk.h: candidates within [-3072, 4864] units of position 0's metric, renormalised
+    every 8 stages), equal to the oracle word for word; the single-batch launch of batch 0 (vd_decode_tg's
+    segment launch: SOFT8 single batches do not run the packed split kernel) too"""
+    nbits = 13_107_264
     n = 2 * nbits
+    nb = 3
     nin = gpu.lib().vd_input_size(opt, n)
-    g = torch.Generator(device="cpu").manual_seed(6)
-    packed = torch.randint(0, 256, (nin + 256,), dtype=torch.uint8, generator=g).to("cuda")
-    before = gpu.split_redecodes()
-    f2 = _single(gpu, opt, packed, nin, n, {"VD_F2": "1"})
-    redec = gpu.split_redecodes() - before
-    p = packed[:nin].cpu().numpy().view(np.int32)
-    ref, ok = vo.decode(opt, p, input_num=n, nthreads=16)
-    got = f2.cpu().numpy().view(ref.dtype)
-    bad = np.flatnonzero(got != ref)
-    assert bad.size == 0, f"{bad.size} of {ref.size} words differ (re-decoded: {redec}), first {bad[:5]}"
-    assert redec > 0
+    stride = (nin + 255) // 256 * 256
+    host = torch.zeros(nb * stride, dtype=torch.uint8)
+    for b in range(nb):
+        host[b * stride:b * stride + nin] = _soft8_pattern(kind, nin, 11 + b)
+    packed = host.to("cuda")
+    pk, ostride, nout = _decode_batched(gpu, opt, packed, stride, n, nb, no_pk=False)
+    single = _single(gpu, opt, packed[:stride], nin, n, {})
+    for b in range(nb):
+        p = host[b * stride:b * stride + nin].numpy().view(np.int32)
+        ref, ok = vo.decode(opt, p, input_num=n, nthreads=16)
+        got = pk[b * ostride:b * ostride + nout].cpu().numpy().view(ref.dtype)
+        bad = np.flatnonzero(got != ref)
+        assert bad.size == 0, f"batch {b}: {bad.size} of {ref.size} words differ, first {bad[:5]}"
+        if b == 0:
+            got1 = single.cpu().numpy().view(ref.dtype)
+            bad = np.flatnonzero(got1 != ref)
+            assert bad.size == 0, f"single launch: {bad.size} of {ref.size} words differ, first {bad[:5]}"
