@@ -5,9 +5,10 @@ One step = one pass of the decode hot path over one batch of each headline workl
 already resident in HBM:
   * HARD  input, M_B32 option       (BASELINE configs[1]: 32M bits, `-i h -m b32`)
   * SOFT8 input, M_B16 option       (BASELINE configs[2]: 32M bits, `-i s8 -m b16`)
-HARD batches on vd_decode_pk (exact-integer tagged metrics in the int16 halves of one word, two chunks
-per wave: 32-bit add, DPP subtract, v_pk_max_u16), SOFT8 batches on vd_decode_tg (the fp32 exact-integer
-tagged core); both reproduce each option's tie rule word for word.
+Both on vd_decode_pk: exact-integer tagged metrics in the int16 halves of one word, two chunks per wave
+(32-bit add, DPP subtract, v_pk_max_u16); HARD with 8-stage history fields, SOFT8 with 2-stage fields and a
+renormalisation every 8 stages (vd_kernel_pk.h); both reproduce each option's tie rule word for word
+(DESIGN.md 4).
 value = decoded bits of both batches (2 x getMessageLen(64e6) = 63,999,872) / step time, summed
 over ranks.  Multi-GPU (BASELINE configs[3]): one process per GPU, each rank decodes its own
 independent batches (weak scaling, no data-path collective; an RCCL all_gather of per-rank
@@ -109,7 +110,7 @@ def parity_block(checks):
     res = {}
     t0 = time.perf_counter()
     for path, opt, inp, gout, n, scale in checks:
-        packed = vo.pack(opt, inp.view(np.float32), scale) if scale is not None else inp.view(vo.in_dtype(opt))
+        packed = vo.pack(opt, inp.view(np.float32), scale, input_num=n) if scale is not None else inp.view(vo.in_dtype(opt))
         ref, ok = vo.decode(opt, packed, input_num=n, nthreads=nt)
         got = gout.view(np.uint8)[:ref.nbytes].view(ref.dtype)
         mism = int(np.count_nonzero(ref != got)) if got.size == ref.size else -1
@@ -156,19 +157,27 @@ N_XCD = 8         # rocprofv3 sums GRBM_GUI_ACTIVE over the 8 XCDs (MI355X_MICRO
 
 def acs_only_ms(name):
     """Instruction-mix ceiling of a workload's kernel: the time per batch of the same batched launch with
-    only the ACS recursion left (tools/vd_ablate 'ACS only' variant: no table build/reads, read-out,
-    loads or traceback; 8 batches per launch as the bench launches them), from the committed ablation log
-    of this round; None if absent."""
-    # (the batched HARD launches run vd_decode_pk since round 4: no ablation of that kernel, no ceiling)
-    key = {"soft8_b16": "tg soft8/b16 ACS only "}.get(name)
+    only the ACS recursion left (tools/vd_pkab 'ACS only' variant: no table build/reads, read-out, loads or
+    traceback; 20 batches per launch), from the committed ablation log of this round; None if absent."""
+    col = {"hard_b32": 0, "soft8_b16": 1}.get(name)
     p = os.path.join(ROOT, "profiles", PMC_ROUND, "ablate_batched.log")
-    if key is None or not os.path.exists(p):
+    if col is None or not os.path.exists(p):
         return None
     with open(p) as f:
         for line in f:
-            if line.startswith(key) and "median" in line:
-                return float(line.split("median")[1].split()[0])
+            if line.startswith("ACS only"):
+                return float(line.split(")")[-1].split()[col])
     return None
+
+
+def valu_model():
+    """Per-opcode VALU cycle model (tools/isa_mix.py): each kernel's steady-state VALU mix per chunk-stage from
+    its ISA, priced with this round's vd_ubench12 issue costs"""
+    p = os.path.join(ROOT, "profiles", PMC_ROUND, "valu_model.json")
+    if os.path.exists(p):
+        with open(p) as f:
+            return json.load(f)
+    return {}
 
 
 def valu_view(pmc, kernel_ms, stages, name, msg_bits):
@@ -181,9 +190,10 @@ def valu_view(pmc, kernel_ms, stages, name, msg_bits):
                      (SIMD-32 model: a wave64 VALU instruction occupies its SIMD for 2 cycles at the
                      least; max/DPP/permlane/bit-field forms take 4 -- profiles/r02/ubench12.log)
       issue_pct_live = the same with the live kernel time at the PMC run's clock
-      cycle_model_pct = 100 * (2 * (SQ_INSTS_VALU_ADD_F32 + _FMA_F32 + _MUL_F32) + 4 * (the other VALU
-                     instructions)) / (1024 * cycles): fp32 add/sub/fma issue in 2 cycles, max, DPP, SDWA,
-                     integer and bit ops in 4 (ubench12.log); _live: at the live kernel time
+      cycle_model_pct = 100 * (VALU cycles the kernel's instruction mix needs per SIMD) / cycles, where the
+                     mix per chunk-stage comes from the kernel's ISA and each opcode's issue cost from this
+                     round's vd_ubench12 (profiles/<round>/valu_model.json, tools/isa_mix.py); _live: at the
+                     live kernel time
       mix ceiling  = the same launch with only the ACS recursion (tools/vd_ablate)."""
     c = pmc.get("counters_mean_per_dispatch", {})
     if not c or "SQ_INSTS_VALU" not in c:
@@ -204,17 +214,21 @@ def valu_view(pmc, kernel_ms, stages, name, msg_bits):
             v["pmc_run_clock_ghz"] = round(ghz, 3)
             v["pmc_run_kernel_ms"] = round(pmc["pmc_run_kernel_ns_median"] * 1e-6, 4)
             v["issue_pct_live"] = round(100.0 * insts * 2 / (N_SIMD * kernel_ms * 1e-3 * ghz * 1e9), 1)
-        if "SQ_INSTS_VALU_ADD_F32" in c:
-            two = sum(c.get(k, 0.0) for k in ("SQ_INSTS_VALU_ADD_F32", "SQ_INSTS_VALU_FMA_F32", "SQ_INSTS_VALU_MUL_F32"))
-            mcyc = 2 * two + 4 * (insts - two)
-            v["cycle_model_pct"] = round(100.0 * mcyc / (N_SIMD * cyc), 1)
-            if ghz:
-                v["cycle_model_pct_live"] = round(100.0 * mcyc / (N_SIMD * kernel_ms * 1e-3 * ghz * 1e9), 1)
+        model = valu_model().get("kernels", {}).get(name)
+        if model and ghz:
+            # VALU cycles the kernel's instruction mix needs per SIMD (tools/isa_mix.py: ISA mix x ubench costs)
+            # against the SIMD cycles the live kernel time gives at the PMC run's clock
+            need = model["valu_cycles_per_chunk_stage"] * stages / N_SIMD
+            v["cycle_model"] = {"valu_cycles_per_chunk_stage": model["valu_cycles_per_chunk_stage"],
+                                "valu_insts_per_chunk_stage_isa": model["valu_per_chunk_stage"],
+                                "source": f"profiles/{PMC_ROUND}/valu_model.json (tools/isa_mix.py)"}
+            v["cycle_model_pct_live"] = round(100.0 * need / (kernel_ms * 1e-3 * ghz * 1e9), 1)
+            v["cycle_model_pct"] = round(100.0 * need / cyc, 1)
     acs = acs_only_ms(name)
     if acs:
         v["mix_ceiling"] = {"acs_only_ms": acs, "gbps": round(msg_bits / (acs * 1e-3) / 1e9, 2),
                             "frac": round(acs / kernel_ms, 3),
-                            "source": f"profiles/{PMC_ROUND}/ablate_batched.log (random input, 8 batches per launch)"}
+                            "source": f"profiles/{PMC_ROUND}/ablate_batched.log (tools/vd_pkab: codeword input, 20 batches per launch)"}
     v["source"] = f"profiles/{PMC_ROUND}/pmc_summary.json"
     return v
 
@@ -400,7 +414,7 @@ def other_configs_side_measurement(dev, sptr, stream, reps=20, keep=None):
         ms = e[0].elapsed_time(e[1]) / reps
         msg = vitdec.lib().vd_message_len(opt, n)
         ber = max(batch_ber(opt, bits, outs, ostride, nout, k, msg)[0] for k in (0, reps - 1))
-        res[name] = {"kernel": vitdec.kernel_name(opt), "kernel_ms": round(ms, 4),
+        res[name] = {"kernel": dec.kernel_for(n, reps), "kernel_ms": round(ms, 4),
                      "gbps": round(msg / (ms * 1e-3) / 1e9, 2), "ber": ber, "batches_per_launch": reps}
         if keep is not None:  # host copies for the parity block: batch 0 and the last batch of the launch
             nin = vitdec.lib().vd_input_size(opt, n)
@@ -437,7 +451,8 @@ def single_launch_side_measurement(batches, stream, sptr, reps=20, keep=None):
         # on the GPU); batch 0 also goes to the oracle in the parity block
         same = [bool(torch.equal(souts[k * b["ostride"]:k * b["ostride"] + nout], b["outs"][k * b["ostride"]:k * b["ostride"] + nout]))
                 for k in range(n)]
-        res[b["name"]] = {"kernel_ms": round(ms, 4), "gbps": round(b["msg"] / (ms * 1e-3) / 1e9, 2), "launches": n,
+        res[b["name"]] = {"kernel": b["dec"].kernel_for(b["input_num"], 1, b["llr"]), "kernel_ms": round(ms, 4),
+                          "gbps": round(b["msg"] / (ms * 1e-3) / 1e9, 2), "launches": n,
                           "equals_batched_launch": f"{sum(same)} of {n} batches"}
         if keep is not None:
             keep.append((f"single_launch.{b['name']}[batch 0]", b["opt"], b["inp"].cpu().numpy(),
@@ -788,7 +803,7 @@ def main():
             ach = alg / (kms[i] * 1e-3) / 1e9
             pmc = pmcs.get(b["name"], {})
             stages = stages_per_launch(b["opt"], b["input_num"])
-            return {"kernel": b["name"] + ": " + vitdec.kernel_name(b["opt"]), "ms": round(kms[i], 4),
+            return {"kernel": b["name"] + ": " + b["dec"].kernel_for(b["input_num"], sizes[0], b["llr"]), "ms": round(kms[i], 4),
                     "launch_ms": round(launch_ms[i], 4), "batches_per_launch": P, "launches": len(sizes),
                     "achieved": round(ach, 2), "frac": round(ach / HBM_PEAK_GBS, 5),
                     "algorithmic_bytes_per_batch": alg, "algorithmic_bytes_per_step_launches": alg * K,
@@ -808,17 +823,17 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "exact integers: HARD in int16 halves (u16x2), SOFT8 in fp32 (int32/int16 tie semantics)",
+            "dtype": "exact integers in int16 halves (u16x2) for HARD and SOFT8 (int32 / int16 tie semantics)",
             "data": f"synthetic: the reference harness chain generated on the GPU bit-exactly (std::mt19937 "
                     f"bits, K=7 (0171,0133) encoder, BPSK + normal_distribution<float> AWGN at {SNR_DB} dB, "
                     f"quantiser scale 40000), seeds (1+2i, 2+2i) for batch i = 2 rank + workload",
             "config": {
                 "workload": "per GPU per step: one 32M-bit HARD batch with the M_B32 option (int32 tie rule) + "
                             "one 32M-bit SOFT8 batch with the M_B16 option (int16 tie rule), BASELINE configs[1]+[2], "
-                            "HARD on vd_decode_pk (exact-integer tagged metrics in the int16 halves of one word, "
-                            "two chunks per wave: v_add_u32, v_sub_u32_dpp, v_pk_max_u16), SOFT8 on vd_decode_tg "
-                            "(fp32 exact-integer tagged core; SOFT8's metric spread does not fit int16 halves with "
-                            "history tags: DESIGN.md 4); each batch uses the reference's 6400-chunk partition",
+                            "both on vd_decode_pk (exact-integer tagged metrics in the int16 halves of one word, "
+                            "two chunks per wave: v_add_u32, v_sub_u32_dpp, v_pk_max_u16; HARD 8-stage history "
+                            "fields, SOFT8 2-stage fields renormalised every 8 stages: DESIGN.md 4); each batch "
+                            "uses the reference's 6400-chunk partition",
                 "n_bits_per_batch": N_BITS,
                 "decoded_bits_per_batch": batches[0]["msg"],
                 "parallelism": f"batch-shard x{world}" if world > 1 else "single GPU (1-rank RCCL group)",
@@ -835,7 +850,7 @@ def main():
                 "kernel_gbps": {b["name"]: round(b["msg"] / (k * 1e-3) / 1e9, 2) for b, k in zip(batches, kms)},
                 "ber": {b["name"]: bers[i] for i, b in enumerate(batches)},
                 "ber_is": "max over the K batches of a launch",
-                "kernels": {b["name"]: vitdec.kernel_name(b["opt"]) for b in batches},
+                "kernels": {b["name"]: b["dec"].kernel_for(b["input_num"], sizes[0], b["llr"]) for b in batches},
             },
             "roofline": {
                 "bound": "valu",

@@ -330,6 +330,22 @@ static unsigned plan_split(vd::Geom& g, int options, const DeviceState* x, int m
     return T.nwg;
 }
 
+// Which kernel and launch form a decode takes (launch_decode and vd_decoder_kernel_name share it):
+// batched launches of HARD/SOFT4/SOFT8/FP32 on vd_decode_pk (two chunks per wave); single batches of
+// HARD/SOFT4/FP32 with chunks of >= kSplitMinWords words on vd_decode_pk's split kernel; the rest on
+// vd_decode_tg (segment launch when plan_split finds a table, else one chunk per wave).
+enum class Form { PkBatched, PkSplit, Tg };
+static Form plan_form(const vd_decoder* d, uint64_t packNum, uint32_t nbatch, bool llr)
+{
+    const int options = d->options;
+    if (nbatch > 1 && d->pk && vd::kChunks % (2 * vd::kWaves) == 0 && pick_pk<false>(options, llr)) return Form::PkBatched;
+    const uint64_t w32 = out_of(options) != 0 ? packNum / 2 : packNum;
+    const bool splitok = nbatch == 1 && d->pk && d->pksplit && d->split && vd::kChunks % vd::kWaves == 0 &&
+                         w32 / vd::kChunks >= (uint64_t)vd::kSplitMinWords;
+    if (splitok && pick_pk<true>(options, llr)) return Form::PkSplit;
+    return Form::Tg;
+}
+
 // llr: in_d holds inputNum float channel values, quantised in the kernel (scale = packer scale).
 // nbatch > 1: batch b at in_d + b * inStride, out_d + b * outStride, all in one launch (never split).
 static int launch_decode(const vd_decoder* d, const void* in_d, void* out_d, size_t inputNum, hipStream_t s,
@@ -359,18 +375,13 @@ static int launch_decode(const vd_decoder* d, const void* in_d, void* out_d, siz
     g.nbatch = nbatch;
     g.inStride = inStride;
     g.outStride = outStride;
-    launch_fn fp = nbatch > 1 && d->pk && g.nchunks % (2 * vd::kWaves) == 0 ? pick_pk<false>(options, llr) : nullptr;
-    if (fp) {  // two chunks per wave: nchunks * nbatch / 8 workgroups
-        fp(in_d, out_d, g, (unsigned)((uint64_t)g.nchunks * nbatch / (2 * vd::kWaves)), s);
+    const Form form = plan_form(d, g.packNum, nbatch, llr);
+    if (form == Form::PkBatched) {  // two chunks per wave: nchunks * nbatch / 8 workgroups
+        pick_pk<false>(options, llr)(in_d, out_d, g, (unsigned)((uint64_t)g.nchunks * nbatch / (2 * vd::kWaves)), s);
         VD_HIP(hipGetLastError());
         return VD_OK;
     }
-    // single batch, chunks long enough to cut: one chunk per wave, cut in two halves (nchunks / 4 workgroups)
-    const uint64_t w32 = out_of(options) != 0 ? g.packNum / 2 : g.packNum;
-    const bool splitok = nbatch == 1 && d->pk && d->pksplit && d->split && g.nchunks % vd::kWaves == 0 &&
-                         w32 / g.nchunks >= (uint64_t)vd::kSplitMinWords;
-    fp = splitok ? pick_pk<true>(options, llr) : nullptr;
-    if (fp) {
+    if (form == Form::PkSplit) {  // single batch: one chunk per wave, cut in two halves (nchunks / 4 workgroups)
         g.stats = d->ds->stats;
         // the last nchunks mod (SIMDs) chunks one per workgroup of 4 waves (8 parts each): with 6400 chunks
         // on 1024 SIMDs every SIMD then runs 6 whole-chunk waves and one short one (vd_kernel_pk.h "split")
@@ -380,7 +391,7 @@ static int launch_decode(const vd_decoder* d, const void* in_d, void* out_d, siz
             g.tailWG = (g.nchunks - tailc) / vd::kWaves;
             grid = g.tailWG + tailc;
         }
-        fp(in_d, out_d, g, grid, s);
+        pick_pk<true>(options, llr)(in_d, out_d, g, grid, s);
         VD_HIP(hipGetLastError());
         return VD_OK;
     }
@@ -410,6 +421,31 @@ int vd_split_redecodes(int device, uint64_t* count)
 }
 const char* vd_last_error(void) { return g_err.c_str(); }
 const char* vd_kernel_name(int options) { return kname(options); }
+
+const char* vd_decoder_kernel_name(vd_decoder* d, size_t inputNum, int nbatch, int llr)
+{
+    static thread_local std::string name;
+    if (!d || nbatch < 1) return "-";
+    static const char* chs[5] = {"HARD", "SOFT4", "SOFT8", "SOFT16", "FP32"};
+    static const char* cores[3] = {"B32", "B16", "F16"};
+    const int o = d->options;
+    const uint64_t packNum = message_len(o, inputNum) / (size_t)bpp_of(o);
+    const std::string args = std::string(llr ? "LLR+" : "") + chs[ch_of(o)] + "," + cores[met_of(o)] + "," +
+                             (out_of(o) ? "O16" : "O32") + ">";
+    vd::Geom g;
+    g.packNum = packNum;
+    g.nchunks = vd::kChunks;
+    switch (plan_form(d, packNum, (uint32_t)nbatch, llr != 0)) {
+    case Form::PkBatched: name = "vd_decode_pk<" + args + " batched: two chunks per wave, int16 halves"; break;
+    case Form::PkSplit: name = "vd_decode_pk<" + args + " split: one chunk per wave cut in two, int16 halves"; break;
+    default:
+        if (nbatch == 1) (void)plan_split(g, o, d->ds, d->split);
+        name = "vd_decode_tg<" + args + (g.seg ? " segment launch: one chunk or piece per wave, fp32 tagged core"
+                                               : " one chunk per wave, fp32 tagged core");
+        if (ch_of(o) == 3) name.replace(name.find("fp32 tagged core"), 16, "int32 tagged patterns");
+    }
+    return name.c_str();
+}
 
 int vd_device_count(void)
 {
@@ -558,9 +594,8 @@ int vd_run_device_batch(vd_decoder* d, const void* input_d, size_t input_stride,
     if (message_len(d->options, inputNum) == 0) return fail(VD_ERR_ARG, "inputNum too small");
     if (nbatch > 1 && output_stride < message_len(d->options, inputNum) / 8)
         return fail(VD_ERR_ARG, "output_stride smaller than the output size: batches would overlap");
-    // input_stride 0 = every batch decodes the same input (broadcast); otherwise the inputs may not overlap
-    if (nbatch > 1 && input_stride != 0 && input_stride < input_size(d->options, inputNum))
-        return fail(VD_ERR_ARG, "input_stride smaller than the input size: batches would overlap");
+    // input_stride: any (0 = every batch decodes the same input); inputs are only read, so overlapping
+    // windows (e.g. sliding) are valid
     if ((uint64_t)vd::kChunks * (uint64_t)nbatch > 0xFFFFFFFFull) return fail(VD_ERR_ARG, "nbatch too large");
     if ((input_stride | output_stride) & 3) return fail(VD_ERR_ARG, "strides must be multiples of 4 bytes");
     if (nbatch == 1) return launch_decode(d, input_d, output_d, inputNum, (hipStream_t)stream);
@@ -609,8 +644,6 @@ int vd_run_device_llr_batch(vd_decoder* d, const float* llr_d, size_t llr_stride
     if (message_len(d->options, inputNum) == 0) return fail(VD_ERR_ARG, "inputNum too small");
     if (nbatch > 1 && output_stride < message_len(d->options, inputNum) / 8)
         return fail(VD_ERR_ARG, "output_stride smaller than the output size: batches would overlap");
-    if (nbatch > 1 && llr_stride < inputNum * sizeof(float) && llr_stride != 0)
-        return fail(VD_ERR_ARG, "llr_stride smaller than the input size: batches would overlap");
     if ((uint64_t)vd::kChunks * (uint64_t)nbatch > 0xFFFFFFFFull) return fail(VD_ERR_ARG, "nbatch too large");
     if ((llr_stride & 15) || (output_stride & 3)) return fail(VD_ERR_ARG, "llr_stride % 16 or output_stride % 4 != 0");
     if (nbatch == 1) return launch_decode(d, llr_d, output_d, inputNum, (hipStream_t)stream, true, scale);

@@ -38,23 +38,25 @@
 // rings in a wave's 5,120 B leave 6 slots each, so a traceback batch traces 5 words per chunk, both chunks'
 // words in one pass (lanes 0..4 chunk A, lanes 32..36 chunk B).
 //
-// Read-out.  J = 8 (HARD): SDWA shifts each half's field bits into byte g of its chunk's ring word.  J = 4
+// Read-out.  Every field clear is (V & ~field) | base as one v_bitop3_b32 (2 cycles; v_and_or_b32 takes 4,
+// profiles/r05/ubench12.log).  J = 8 (HARD): SDWA shifts each half's field bits into byte g of its chunk's ring word.  J = 4
 // (SOFT4 / FP32): nibble g of the ring word; field pairs are gathered as c = (V >> 1) of the even field,
 // bfi(0x00F000F0, V << 3, c) of the odd one (chunk A's two fields in byte 0, chunk B's in byte 2), and at
 // the block end four v_perm_b32 turn the four pair words into the two ring words.
 // J = 2 (SOFT8): after a field F = 4 + h is odd, its take-bits d = bits 1, 2.  x = V & 0x00060006 (both
-// halves), V = (V ^ x) + 0x00030003 puts F back to 4 (one v_xad_u32; every fourth field the constant also
-// renormalises: VBASE - 0x00010001 - (V of position 0 & ~7 in each half), on the scalar unit), and
-// v_lshl_or_b32 collects d into bits 2g of two pair words (fields 0..7 and 8..15; chunk A low, chunk B high
-// half) that are the block's two ring words as they stand -- 3 VALU per field for both chunks.
+// halves, v_and_b32), V = (V & ~7) | 4 per half (v_bitop3_b32) puts F back to 4; every fourth field instead
+// V = (V ^ x) + VBASE - 0x00010001 - (V of position 0 & ~7 in each half) (v_xad_u32, the constant on the
+// scalar unit) clears and renormalises at once; v_lshl_or_b32 collects d into bits 2g of two pair words
+// (fields 0..7 and 8..15; chunk A low, chunk B high half) that are the block's two ring words as they stand --
+// 3 VALU per field for both chunks, 8 cycles (v_and_b32 and v_bitop3_b32 issue in 2, profiles/r05/ubench12.log).
 // Ring and traceback (SOFT8).  The ring is indexed by p' = rotl6(p, 1), where the two stages of a field
 // (t0 even, t0 + 1) flip position bits q' = t0 % 6 and t0 % 6 + 1 (never wrapping).  Tracing back is then
 // position arithmetic: from p' = 0 (state 0) at a block end, each field back is p' ^= d << (t0 % 6), and the
 // field's two decoded bits are bits t0 % 6, t0 % 6 + 1 of the new p' (the stored bit of an M_B32 phase-0 stage
 // in the upper position half, an own-won tag, is complemented once per block so that every stored bit is a
 // take-bit).  A lane keeps its LDS read address A = slot | 4 p' (ring slots 256-B aligned: the ring leads the
-// wave's LDS), so a step is one ds_read_u8 at a constant offset, v_bfe_u32, v_lshlrev_b32 (the lane's phase)
-// and v_xor_b32: 32 dependent steps per word (tools/pk2_model.py replays the scheme against the reference).
+// wave's LDS), so a step is one ds_read_u8_d16_hi at a constant offset and three 2-cycle VALU ops (pk2_traceback):
+// 32 dependent steps per word (tools/pk2_model.py replays the scheme against the reference).
 #pragma once
 #include "vd_kernel_tg.h"
 
@@ -136,22 +138,36 @@ static_assert(PkLds<8, true>::TBS == 5 && kWaves * PkLds<8, true>::WAVE * 4 <= 2
 // convergence block k + 2 is the next slot, +512 B) | 2 for chunk B's half; z[r] = 2 + the position bit of the
 // first stage of convergence-block field g (g % 3 = r); the emit block's field g has z[(g + 2) % 3].
 template <int CORE>
-__device__ __forceinline__ uint32_t pk2_traceback(uint32_t A, const uint32_t (&z)[3])
+__device__ __forceinline__ uint32_t pk2_traceback(uint32_t A, const uint32_t (&z)[3], const uint32_t (&zm)[3], uint32_t rho,
+                                                  uint32_t mlo)
 {
-    typedef const __attribute__((address_space(3))) uint8_t* lp8;
-    uint32_t nat = 0;
+    uint32_t nat = 0, B = 0;
+    // a step: the byte holding field g loaded into bits 16..23 (ds_read_u8_d16_hi: its pair at 16 + 2 (g % 4)),
+    // shifted right onto the lane's position bits z (v_sub_u32 + v_lshrrev_b32) and XORed in under the mask
+    // zm = 3 << z (v_bitop3_b32): 6 cycles of 2-cycle ops where v_bfe / v_lshlrev / v_xor took 10
     auto step = [&](auto EMc, auto Gc) {
         constexpr bool EM = decltype(EMc)::value;
         constexpr int g = decltype(Gc)::value;
         constexpr int off = (EM ? 0 : 512) + 256 * (g / 8) + (g % 8) / 4;
-        const uint32_t B = ((lp8)(uintptr_t)A)[off];
-        const uint32_t d = __builtin_amdgcn_ubfe(B, 2 * (g % 4), 2);
-        const uint32_t zz = z[EM ? (g + 2) % 3 : g % 3];
-        A ^= d << zz;
-        if constexpr (EM) nat |= __builtin_amdgcn_ubfe(A, zz, 2) << (2 * g);  // bit s <-> block stage s
+        constexpr int r = EM ? (g + 2) % 3 : g % 3;
+        // (one statement: the compiler would otherwise hoist the 12 shift amounts of a pass into registers)
+        uint32_t t;
+        asm volatile("ds_read_u8_d16_hi %[b], %[a] offset:%[o]\n\tv_sub_u32 %[t], %[k], %[z]\n\ts_waitcnt lgkmcnt(0)\n\t"
+                     "v_lshrrev_b32 %[t], %[t], %[b]\n\tv_bitop3_b32 %[a], %[a], %[t], %[m] bitop3:0x78"  // A ^ (t & zm)
+                     : [a] "+v"(A), [b] "+v"(B), [t] "=&v"(t)
+                     : [o] "n"(off), [k] "n"(16 + 2 * (g % 4)), [z] "v"(z[r]), [m] "v"(zm[r]) : "memory");
+        // emit block: after fields 3m + 3, 3m + 2, 3m + 1 (m = 4 .. 0) the address bits 2..7 hold their three
+        // decoded pairs (each field sets the pair at its own z, and the z cycle has period 3); snapshot them
+        // into bits 6m + 2 .. 6m + 7; field 0's pair goes to bits 0, 1
+        if constexpr (EM && g % 3 == 1) nat |= (A & 0xFCu) << (2 * g - 2);
+        if constexpr (EM && g == 0) nat |= __builtin_amdgcn_ubfe(A, z[r], 2);
     };
     sfor<16>([&](auto I) { step(std::false_type{}, std::integral_constant<int, 15 - decltype(I)::value>{}); });
     sfor<16>([&](auto I) { step(std::true_type{}, std::integral_constant<int, 15 - decltype(I)::value>{}); });
+    // each 6-bit snapshot holds fields 3m + 1, 3m + 2, 3m + 3 at bits rho, rho + 2, rho + 4 (mod 6): rotate every
+    // group right by rho (mlo: the groups' low 6 - rho bits) so that field g's pair lands at bits 2g, 2g + 1
+    const uint32_t grp = nat & ~3u;
+    nat = (nat & 3u) | ((grp >> rho) & mlo) | ((grp << (6u - rho)) & ~mlo);  // v_bfi_b32
     return __builtin_bitreverse32(nat);  // word bit i <-> stage 63+32k-i
 }
 
@@ -335,17 +351,19 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(SPL
                             "s_and_b32 %[sr], %[sr], 0xfff8fff8\n\ts_sub_u32 %[sr], %[vb], %[sr]\n\t"
                             "v_xad_u32 %[V], %[V], %[x], %[sr]"
                             : [V] "+{v60}"(V), [x] "=&v"(x), [sr] "=&s"(sr) : [vb] "n"(VBASE - 0x10001u) : "scc");
-                    else
-                        asm("v_and_b32 %[x], 0x60006, %[V]\n\tv_xad_u32 %[V], %[V], %[x], %[c]"
-                            : [V] "+{v60}"(V), [x] "=&v"(x) : [c] "s"(0x30003u));
+                    else  // the clear as (V & ~7) | 4 per half: v_bitop3_b32 (2 cycles; v_xad_u32 takes 4)
+                        asm("v_and_b32 %[x], 0x60006, %[V]\n\tv_bitop3_b32 %[V], %[V], %[m], %[c] bitop3:0xea"
+                            : [V] "+{v60}"(V), [x] "=&v"(x) : [m] "v"(0xFFF8FFF8u), [c] "s"(0x40004u));
+                    // one v_lshl_or_b32 per field (left to itself the compiler paired fields as two shifts
+                    // and a v_or3_b32: 1.5 ops per field)
                     if constexpr (h == 0) cw[g / 8] = x >> 1;
-                    else cw[g / 8] = (x << (2 * h - 1)) | cw[g / 8];
+                    else asm("v_lshl_or_b32 %0, %1, %2, %0" : "+v"(cw[g / 8]) : "v"(x), "n"(2 * h - 1));
                 } else if constexpr (J == 8) {
                     // bits 1..8 of each half into byte g of its ring word (SDWA)
 #define VD_PK_RO(SEL, UNUSED)                                                                                \
     "v_lshrrev_b32_sdwa %[wa], 1, %[V] dst_sel:" SEL " dst_unused:" UNUSED " src0_sel:DWORD src1_sel:DWORD\n\t"  \
     "v_lshrrev_b32_sdwa %[wb], 1, %[V] dst_sel:" SEL " dst_unused:" UNUSED " src0_sel:DWORD src1_sel:WORD_1\n\t" \
-    "v_and_or_b32 %[V], %[V], %[fnm], %[fhf]"
+    "v_bitop3_b32 %[V], %[V], %[fnm], %[fhf] bitop3:0xea"
                     if constexpr (g == 0)
                         asm(VD_PK_RO("BYTE_0", "UNUSED_PAD") : [V] "+{v60}"(V), [wa] "=&v"(wA), [wb] "=&v"(wB) : VD_PK_IN);
                     else if constexpr (g == 1)
@@ -360,8 +378,8 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(SPL
                     // bits 1..4 of each half: the even field's as V >> 1, the odd field's (V << 3) into the
                     // high nibbles of the pair word (chunk A byte 0, chunk B byte 2)
                     constexpr uint32_t HN = 0x00F000F0u;
-#define VD_PK_RO4E "v_lshrrev_b32 %[c], 1, %[V]\n\tv_and_or_b32 %[V], %[V], %[fnm], %[fhf]"
-#define VD_PK_RO4O "v_lshlrev_b32 %[t], 3, %[V]\n\tv_and_or_b32 %[V], %[V], %[fnm], %[fhf]\n\tv_bfi_b32 %[c], %[hn], %[t], %[c]"
+#define VD_PK_RO4E "v_lshrrev_b32 %[c], 1, %[V]\n\tv_bitop3_b32 %[V], %[V], %[fnm], %[fhf] bitop3:0xea"
+#define VD_PK_RO4O "v_lshlrev_b32 %[t], 3, %[V]\n\tv_bitop3_b32 %[V], %[V], %[fnm], %[fhf] bitop3:0xea\n\tv_bfi_b32 %[c], %[hn], %[t], %[c]"
                     uint32_t t;
                     if constexpr (g % 2 == 0)
                         asm(VD_PK_RO4E : [V] "+{v60}"(V), [c] "=&v"(cw[g / 2]) : VD_PK_IN);
@@ -428,7 +446,11 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(SPL
                     // 2 ((k + 2 + g) % 3)
                     const uint32_t u = (k + 2u) % 3u;
                     const uint32_t z[3] = {2u * u + 2u, u == 2u ? 2u : 2u * u + 4u, u == 0u ? 6u : 2u * u};
-                    w = pk2_traceback<CORE>(tbA2, z);
+                    // emit snapshots: rotate each 6-bit group right by 2u (pk2_traceback)
+                    const uint32_t rho = 2u * u;
+                    const uint32_t mlo = rho == 0u ? 0xFFFFFFFCu : rho == 2u ? 0x3CF3CF3Cu : 0x0C30C30Cu;
+                    const uint32_t zm[3] = {3u << z[0], 3u << z[1], 3u << z[2]};
+                    w = pk2_traceback<CORE>(tbA2, z, zm, rho, mlo);
                 } else {
                     const TbC tc = tb_direct<(J < 6 ? 6 : J), CORE == B32>((int)k);
                     w = traceback_word_tg<J, CORE == B32>(tbring, (tbl + 1u) * 256u, tc);

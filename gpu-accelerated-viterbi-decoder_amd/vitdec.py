@@ -45,7 +45,8 @@ EXPORTS = ["vd_options_valid", "vd_input_size", "vd_message_len", "vd_output_siz
            "vd_simulate_host", "vd_count_errors", "vd_last_error", "vd_device_count", "vd_kernel_name",
            "vd_pack_device", "vd_run_device_llr", "vd_run_llr", "vd_host_alloc", "vd_host_free",
            "vd_run_stream", "vd_channel_device", "vd_simulate_device", "vd_mt_state_after", "vd_split_redecodes",
-           "vd_set_guard_check", "vd_guard_violations", "vd_run_device_llr_batch", "vd_build_info"]
+           "vd_set_guard_check", "vd_guard_violations", "vd_run_device_llr_batch", "vd_build_info",
+           "vd_decoder_kernel_name"]
 
 
 class VitdecError(RuntimeError):
@@ -64,6 +65,9 @@ def lib():
         raise VitdecError(f"{LIB_PATH} not built: run `make -C {_HERE}` (or __graft_entry__.build())")
     L = ctypes.CDLL(LIB_PATH)
     if not os.environ.get("VITDEC_LIB"):  # the product library must be built from the sources in this tree
+        if not hasattr(L, "vd_build_info"):
+            raise VitdecError(f"{LIB_PATH} predates the build record (no vd_build_info): rebuild it with "
+                              f"`make -C {_HERE}`")
         L.vd_build_info.restype = ctypes.c_char_p
         stale = build_mismatch(L.vd_build_info().decode())
         if stale:
@@ -89,7 +93,8 @@ def lib():
            "vd_run_device_llr": ([vp, vp, vp, sz, f, vp], None),
            "vd_run_llr": ([vp, vp, vp, sz, f, ctypes.POINTER(f)], None),
            "vd_run_device_llr_batch": ([vp, vp, sz, vp, sz, sz, f, ctypes.c_int, vp], None),
-           "vd_kernel_name": ([i], ctypes.c_char_p)}
+           "vd_kernel_name": ([i], ctypes.c_char_p),
+           "vd_decoder_kernel_name": ([vp, sz, i, i], ctypes.c_char_p)}
     for name, (args, res) in sig.items():
         if not hasattr(L, name):
             if os.environ.get("VITDEC_LIB"):  # an earlier round's build in a same-box A/B: fewer entry points
@@ -231,6 +236,11 @@ class ViterbiCUDA:
         same input each time) -> output_ptr + b * output_stride bytes (vd_run_device_batch)."""
         _check(lib().vd_run_device_batch(self._h, ctypes.c_void_p(input_ptr), input_stride, ctypes.c_void_p(output_ptr),
                                          output_stride, inputNum, nbatch, ctypes.c_void_p(stream)))
+
+    def kernel_for(self, inputNum, nbatch=1, llr=False):
+        """the kernel and launch form this decoder runs for nbatch batches of inputNum values
+        (vd_decoder_kernel_name: follows VD_NO_PK / VD_PK_SPLIT / VD_NO_SPLIT as read at creation)"""
+        return lib().vd_decoder_kernel_name(self._h, inputNum, nbatch, 1 if llr else 0).decode()
 
     def set_guard_check(self, enable=True):
         """LDS guard words around every wave's table and ring, counted at kernel exit when overwritten

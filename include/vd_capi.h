@@ -76,9 +76,10 @@ int vd_run(vd_decoder* dec, const void* input_h, void* output_h, size_t inputNum
 int vd_run_device(vd_decoder* dec, const void* input_d, void* output_d, size_t inputNum, void* stream);
 
 /* nbatch independent batches of inputNum encoded values each in ONE launch (new; for batched callers):
- * batch b reads input_d + b * input_stride bytes and writes output_d + b * output_stride bytes.  input_stride
- * is 0 (broadcast: every batch decodes the same input) or >= vd_input_size; output_stride >= vd_output_size
- * unless nbatch == 1 (else VD_ERR_ARG: overlapping batches).  Each batch decodes exactly
+ * batch b reads input_d + b * input_stride bytes and writes output_d + b * output_stride bytes.  Inputs are
+ * only read, so input_stride is free (0: every batch decodes the same input; smaller than vd_input_size:
+ * overlapping windows); output_stride >= vd_output_size unless nbatch == 1 (else VD_ERR_ARG: overlapping
+ * outputs).  Each batch decodes exactly
  * as vd_run_device would (the reference's 6400-chunk partition per batch); one launch fills the GPU's
  * tail with the next batch's chunks.  Strides are multiples of 4 bytes; device pointers as above. */
 int vd_run_device_batch(vd_decoder* dec, const void* input_d, size_t input_stride, void* output_d,
@@ -123,7 +124,7 @@ int vd_run_device_llr(vd_decoder* dec, const float* llr_d, void* output_d, size_
                       void* stream);
 /* nbatch independent batches of inputNum device floats in one launch (as vd_run_device_batch): batch b
  * reads llr_d + b * llr_stride bytes and writes output_d + b * output_stride bytes (strides multiples
- * of 16 and 4 bytes; llr_stride 0 = broadcast or >= 4 * inputNum, output_stride as vd_run_device_batch). */
+ * of 16 and 4 bytes; llr_stride free as input_stride, output_stride as vd_run_device_batch). */
 int vd_run_device_llr_batch(vd_decoder* dec, const float* llr_d, size_t llr_stride, void* output_d,
                             size_t output_stride, size_t inputNum, float scale, int nbatch, void* stream);
 /* Blocking host-to-host variant (H2D of the floats, fused decode, D2H); kernel_ms as in vd_run. */
@@ -167,8 +168,12 @@ int vd_set_guard_check(vd_decoder* dec, int enable);
 int vd_guard_violations(vd_decoder* dec, uint64_t* count);
 const char* vd_last_error(void);
 int vd_device_count(void);
-/* last decode kernel's name and grid, for profilers (static strings) */
+/* the kernels an option combination can run, for profilers (static strings) */
 const char* vd_kernel_name(int options);
+/* the kernel and launch form this decoder takes for a decode of inputNum encoded values in nbatch batches
+ * (vd_run_device: nbatch 1; vd_run_device_batch: nbatch) of packed (llr 0) or float (llr 1) input, under
+ * the knobs read at vd_create (VD_NO_PK, VD_PK_SPLIT, VD_NO_SPLIT); valid until the thread's next call */
+const char* vd_decoder_kernel_name(vd_decoder* dec, size_t inputNum, int nbatch, int llr);
 /* build record: "<16 hex digits of the SHA-256 of the concatenated sources> <their paths, relative to the
  * package directory>"; the Python binding refuses a library whose sources have changed since (stale build) */
 const char* vd_build_info(void);

@@ -96,11 +96,29 @@ def simulate(opt, n_bits, snr, bit_seed, noise_seed, noiseless=False):
     return bits, packed
 
 
+def _c_buffer(a, what):
+    """a C-contiguous numpy array (the C side reads it through one pointer)"""
+    if not isinstance(a, np.ndarray):
+        raise ValueError(f"{what}: a numpy array is required, got {type(a).__name__}")
+    if not a.flags.c_contiguous:
+        raise ValueError(f"{what}: the array must be C-contiguous")
+    return a
+
+
 def decode(opt, packed, input_num=None, nchunks=6400, b16_policy=0, nthreads=None):
-    """Decode like ViterbiCUDA<opt>::run; returns (decPack_t array, range_ok)."""
+    """Decode like ViterbiCUDA<opt>::run; returns (decPack_t array, range_ok).
+
+    Raises ValueError when `packed` holds fewer than input_size(opt, input_num) bytes: the C decoder reads
+    that many, and a short buffer would be read past its end (round 4: a parity slice sized in packed words
+    instead of bytes crashed the bench's parity block in decode_chunk)."""
+    _c_buffer(packed, "decode")
     if input_num is None:
         per = {HARD: 32, SOFT4: 8, SOFT8: 4, SOFT16: 2, FP32: 1}[opt & 0xF]
         input_num = packed.size * per
+    need = input_size(opt, input_num)
+    if packed.nbytes < need:
+        raise ValueError(f"decode: the input holds {packed.nbytes} bytes, option 0x{opt:x} with inputNum {input_num} "
+                         f"reads {need}")
     out = np.zeros(output_size(opt, input_num) // np.dtype(out_dtype(opt)).itemsize, dtype=out_dtype(opt))
     if nthreads is None:
         nthreads = min(8, os.cpu_count() or 1)
@@ -109,8 +127,16 @@ def decode(opt, packed, input_num=None, nchunks=6400, b16_policy=0, nthreads=Non
     return out, rc == 0
 
 
-def pack(opt, values, scale=40000.0):
-    """SoftDecisionPacker(channel, scale) on float32 channel values (viterbiDF.h:98-167)."""
+def pack(opt, values, scale=40000.0, input_num=None):
+    """SoftDecisionPacker(channel, scale) on float32 channel values (viterbiDF.h:98-167).
+
+    input_num: the channel values to pack (default: all of `values`); ValueError when `values` holds fewer."""
+    if not isinstance(values, np.ndarray):
+        raise ValueError(f"pack: a numpy array is required, got {type(values).__name__}")
+    if input_num is not None:
+        if values.size < input_num:
+            raise ValueError(f"pack: {values.size} channel values given, inputNum {input_num}")
+        values = values.reshape(-1)[:input_num]
     v = np.ascontiguousarray(values, dtype=np.float32)
     nbytes = input_size(opt, v.size)
     out = np.zeros((nbytes + 3) // 4, dtype=in_dtype(opt))

@@ -141,19 +141,33 @@ print(json.dumps(res))
 """
 
 
+def scratch_state():
+    """(usable, why): the scratch library exists and its BUILD_RECORD (tools/scc_scratch.sh) matches this tree's
+    product sources -- a stale build is never loaded"""
+    import vitdec
+    rec = os.path.join(os.path.dirname(SCRATCH_LIB), "BUILD_RECORD")
+    if not os.path.exists(SCRATCH_LIB) or not os.path.exists(rec):
+        return False, f"{SCRATCH_LIB} not built (tools/scc_scratch.sh; __graft_entry__.build() runs it)"
+    stale = vitdec.build_mismatch(open(rec).read().strip())
+    if stale:
+        return False, f"{SCRATCH_LIB} is stale ({stale}): rebuild it with tools/scc_scratch.sh"
+    return True, ""
+
+
 @pytest.mark.gpu
 def test_guard_check_catches_the_round2_scc_clobber(gpu):
     """The scratch library (renormalisation asm without "scc" clobber) through the guard check: the check
-    reports overwritten LDS guards, i.e. test_guards_* would fail on that build."""
-    if not os.path.exists(SCRATCH_LIB):
-        pytest.skip(f"{SCRATCH_LIB} not built (tools/scc_scratch.sh): informational test")
-    env = dict(os.environ, VD_ROOT=ROOT, VITDEC_LIB=SCRATCH_LIB)
+    reports overwritten LDS guards, i.e. test_guards_* would fail on that build.  The scratch copy is made
+    from this tree's sources (its build record must match them, or the test skips without loading it), and
+    its decodes run on vd_decode_tg (VD_NO_PK=1), the kernel whose asm the copy breaks."""
+    ok, why = scratch_state()
+    if not ok:
+        pytest.skip(why)
+    env = dict(os.environ, VD_ROOT=ROOT, VITDEC_LIB=SCRATCH_LIB, VD_NO_PK="1")
     r = subprocess.run([sys.executable, "-c", _SCRATCH], capture_output=True, text=True, timeout=180, env=env)
     assert r.returncode == 0, r.stderr[-3000:]
     res = json.loads(r.stdout.strip().splitlines()[-1])
     print(res)
-    # Whether the bug shows depends on the compiler keeping a branch condition in SCC across the asm without
-    # the clobber (tests/test_asm_lint.py scans the ISA for that); a compiler that does not leaves nothing for
-    # the guard check to find, which says nothing about the product: informational then, not a failure.
-    if not any(v["guard_violations"] > 0 for v in res.values()):
-        pytest.skip(f"this compiler's scratch build reads no SCC after the renormalisation: nothing to catch ({res})")
+    # tests/test_asm_lint.py shows on the CPU that this compiler's scratch ISA branches on the subtraction's
+    # borrow; the guard check must then see the consequence (round 4: it did).  No violation is a failure.
+    assert any(v["guard_violations"] > 0 for v in res.values()), f"the guard check caught nothing: {res}"

@@ -137,3 +137,24 @@ def test_packer_matches_harness_pipeline(vo, ch):
         vals[2 * i] = 1.0 if bin(reg & 0o171).count("1") & 1 else -1.0
         vals[2 * i + 1] = 1.0 if bin(reg & 0o133).count("1") & 1 else -1.0
     assert np.array_equal(vo.pack(ch, vals, 40000.0).view(np.uint32), packed.view(np.uint32))
+
+
+def test_short_buffers_raise(vo):
+    """The wrapper refuses inputs shorter than the C side reads (round 4: a parity slice sized in packed words
+    instead of bytes made decode_chunk read past the buffer and crash): a ValueError, not a read past the end."""
+    opt = vo.SOFT8 | vo.M_B16
+    n = 2 * 100_000
+    bits, packed = vo.simulate(opt, n // 2, 1.0, 3, 4)
+    ref, ok = vo.decode(opt, packed, input_num=n)
+    assert ok and ref.size > 0
+    short = packed[:packed.size // 4]  # the round-4 mistake: a quarter of the bytes
+    with pytest.raises(ValueError, match="reads"):
+        vo.decode(opt, short, input_num=n)
+    with pytest.raises(ValueError, match="C-contiguous"):
+        vo.decode(opt, np.repeat(packed, 2)[::2], input_num=n)
+    with pytest.raises(ValueError):
+        vo.decode(opt, list(packed), input_num=n)
+    vals = np.zeros(n, dtype=np.float32)
+    assert vo.pack(opt, vals, 40000.0, input_num=n).nbytes == vo.input_size(opt, n)
+    with pytest.raises(ValueError, match="inputNum"):
+        vo.pack(opt, vals[:n // 2], 40000.0, input_num=n)

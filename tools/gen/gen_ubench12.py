@@ -15,7 +15,16 @@ OPS = {"add_f32": "v_add_f32 {d}, {d}, v40", "sub_f32": "v_sub_f32 {d}, {d}, v40
        "lshr_sdwa": "v_lshrrev_b32_sdwa {d}, 1, {d} dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD",
        "bfe_u32": "v_bfe_u32 {d}, {d}, 1, 8", "cvt_f32_i32": "v_cvt_f32_i32 {d}, {d}",
        "add3_u32": "v_add3_u32 {d}, {d}, v40, v41", "pk_max_u16": "v_pk_max_u16 {d}, {d}, v40",
-       "pk_max_i16": "v_pk_max_i16 {d}, {d}, v40", "pk_add_u16": "v_pk_add_u16 {d}, {d}, v40"}
+       "pk_max_i16": "v_pk_max_i16 {d}, {d}, v40", "pk_add_u16": "v_pk_add_u16 {d}, {d}, v40",
+       # the packed kernels' other opcodes (vd_kernel_pk.h read-out, traceback, table build)
+       "sub_u32": "v_sub_u32 {d}, {d}, v40", "and_b32": "v_and_b32 {d}, 0x60006, {d}",
+       "xad_u32": "v_xad_u32 {d}, {d}, v40, v41", "lshl_or_b32": "v_lshl_or_b32 {d}, {d}, 3, v40",
+       "or3_b32": "v_or3_b32 {d}, {d}, v40, v41", "xor_b32": "v_xor_b32 {d}, {d}, v40",
+       "lshlrev_b32": "v_lshlrev_b32 {d}, 3, {d}", "lshrrev_b32": "v_lshrrev_b32 {d}, 3, {d}",
+       "bitop3_b32": "v_bitop3_b32 {d}, {d}, v40, v41 bitop3:0x96", "lshl_add_u32": "v_lshl_add_u32 {d}, {d}, 3, v40",
+       "bfi_b32": "v_bfi_b32 {d}, v40, {d}, v41", "perm_b32": "v_perm_b32 {d}, {d}, v40, v41",
+       "mul_u32_u24": "v_mul_u32_u24 {d}, {d}, v40", "cndmask_b32": "v_cndmask_b32 {d}, {d}, v40, vcc",
+       "readfirstlane": "v_readfirstlane_b32 s20, {d}"}
 PK = {"pk_add_f32": "v_pk_add_f32 v[{a}:{b}], v[{a}:{b}], v[40:41]",
       "pk_fma_f32": "v_pk_fma_f32 v[{a}:{b}], v[{a}:{b}], v[40:41], v[40:41]",
       "permlane32_swap": "v_permlane32_swap_b32 v{a}, v{b}", "permlane16_swap": "v_permlane16_swap_b32 v{a}, v{b}"}
@@ -80,7 +89,7 @@ for k in ["pk16 dpp (2 chunks)", "pk16 plain (2 chunks)", "pk32 dpp (2 chunks)",
     V.append((f"stage {k} x2 chains per 2 states", stage(k, 2), 48))
 for k in ["2op pk f32 (pair)", "3op pk f32 (pair)", "inlane pk (pair)"]:
     V.append((f"stage {k} per state", stage(k, 2), 48))
-CLB = ','.join(f'"v{i}"' for i in list(range(10, 26)) + [40, 41]) + ', "vcc"'
+CLB = ','.join(f'"v{i}"' for i in list(range(10, 26)) + [40, 41]) + ', "vcc", "s20"'
 src = ['// generated by tools/gen/gen_ubench12.py -- do not edit', '#include <hip/hip_runtime.h>', '#include <cstdio>',
        '#include <vector>', '#include <algorithm>',
        '#define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP %s\\n", hipGetErrorString(e)); return 1; } } while (0)']

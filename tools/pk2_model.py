@@ -141,6 +141,31 @@ def trace_word(ring, k):
     return bits
 
 
+def trace_word_kernel(ring, k):
+    """the kernel's form of trace_word (vd_kernel_pk.h pk2_traceback): the lane's LDS address A = 4 p', the
+    per-lane shifts z[r] of the convergence block's fields, the emit block's pairs collected as 6-bit
+    snapshots after fields 13, 10, 7, 4, 1 and rotated right by rho = 2u per group; returns the output word"""
+    u = (k + 2) % 3
+    z = [2 * ((u + r) % 3) + 2 for r in range(3)]
+    A = 0
+    nat = 0
+    for blk, EM in ((k + 2, False), (k + 1, True)):
+        for g in range(15, -1, -1):
+            d = ring[16 * blk + g][A >> 2]
+            zz = z[(g + 2) % 3] if EM else z[g % 3]
+            A ^= d << zz
+            if EM and g % 3 == 1:
+                nat |= ((A >> 2) & 63) << (2 * g)
+            if EM and g == 0:
+                nat |= (A >> zz) & 3
+    rho = 2 * u
+    mlo = {0: 0xFFFFFFFC, 2: 0x3CF3CF3C, 4: 0x0C30C30C}[rho]
+    grp = nat & ~3 & 0xFFFFFFFF
+    a, b = grp >> rho, (grp << (6 - rho)) & 0xFFFFFFFF
+    nat = (nat & 3) | (a & mlo) | (b & ~mlo & 0xFFFFFFFF)
+    return int("{:032b}".format(nat)[::-1], 2)  # bitreverse: word bit i <-> stage 63 + 32k - i
+
+
 def run(AB, core):
     dec = ref_acs(AB, core)
     ring, lo, hi, spread = model(AB, core)
@@ -151,8 +176,10 @@ def run(AB, core):
     for k in range(nwords):
         a = trace_word(ring, k)
         b = ref_traceback(dec, 32 * k + 95, 64)
+        w = trace_word_kernel(ring, k)
         for t in range(32 * k + 32, 32 * k + 64):
             bad += a[t] != b[t]
+            bad += ((w >> (63 + 32 * k - t)) & 1) != b[t]
     return bad, lo, hi, spread
 
 

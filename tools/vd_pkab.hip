@@ -1,0 +1,131 @@
+// vd_pkab.hip -- timing-only A/B of vd_decode_pk variants in batched launches (not part of the product): the
+// bench's timed region (K distinct resident 32M-bit batches per launch) for HARD/b32 (K=7 codeword through a
+// BSC, p = 0.04) and SOFT8/b16 (BPSK codeword + Gaussian noise at Eb/N0 2 dB, quantised like
+// SoftDecisionPacker(SOFT8)).  Variants alternate round by round with a rotating order; every exact variant's
+// words are compared with variant 0's (last batch).  Component ablations (ABL bits, vd_kernel_tg.h) give
+// wrong words by design and are labelled so.
+// Usage: vd_pkab [rounds] [batches per launch]
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstdlib>
+#include <cmath>
+#include <random>
+#include <vector>
+#include <algorithm>
+#include "../gpu-accelerated-viterbi-decoder_amd/csrc/vd_kernel_pk.h"
+#define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP error %s at %d\n", hipGetErrorString(e), __LINE__); exit(1); } } while (0)
+using KFn = void (*)(const void*, void*, vd::Geom);
+template <int CH, int CORE, int ABL, int NW = 8>
+constexpr KFn pk() { return (KFn)vd::vd_decode_pk<CH, CORE, 32, false, NW, ABL>; }
+struct Variant { const char* name; KFn hard, soft8; bool exact; };
+#ifndef VD_PKAB_VARIANTS
+#define VD_PKAB_VARIANTS                                                                                              \
+    {"full", pk<vd::HARD, vd::B32, 0>(), pk<vd::SOFT8, vd::B16, 0>(), true},                                           \
+    {"ACS only (ablation)", pk<vd::HARD, vd::B32, vd::kAblAcsOnly>(), pk<vd::SOFT8, vd::B16, vd::kAblAcsOnly>(), false}, \
+    {"-traceback (ablation)", pk<vd::HARD, vd::B32, vd::kAblNoTraceback>(), pk<vd::SOFT8, vd::B16, vd::kAblNoTraceback>(), false}, \
+    {"-read-out (ablation)", pk<vd::HARD, vd::B32, vd::kAblNoReadout>(), pk<vd::SOFT8, vd::B16, vd::kAblNoReadout>(), false}, \
+    {"-table build (ablation)", pk<vd::HARD, vd::B32, vd::kAblNoTabBuild>(), pk<vd::SOFT8, vd::B16, vd::kAblNoTabBuild>(), false}, \
+    {"-table reads (ablation)", pk<vd::HARD, vd::B32, vd::kAblNoTabReads>(), pk<vd::SOFT8, vd::B16, vd::kAblNoTabReads>(), false}, \
+    {"-input loads (ablation)", pk<vd::HARD, vd::B32, vd::kAblNoLoads>(), pk<vd::SOFT8, vd::B16, vd::kAblNoLoads>(), false}, \
+    {"7 waves/SIMD, 6 words per traceback", pk<vd::HARD, vd::B32, 0, 7>(), pk<vd::SOFT8, vd::B16, 0, 7>(), true},      \
+    {"6 waves/SIMD, 8 words per traceback", pk<vd::HARD, vd::B32, 0, 6>(), pk<vd::SOFT8, vd::B16, 0, 6>(), true},
+#endif
+
+static double median(std::vector<float> v)
+{
+    std::sort(v.begin(), v.end());
+    return v.empty() ? 0.0 : v[v.size() / 2];
+}
+
+int main(int argc, char** argv)
+{
+    const int rounds = argc > 1 ? atoi(argv[1]) : 6, K = argc > 2 ? atoi(argv[2]) : 20;
+    const size_t N = 32000000;  // coded stages per batch (the bench's 32M-bit input)
+    std::mt19937 rng(7);
+    std::vector<uint8_t> o0(N), o1(N);
+    uint32_t reg = 0;
+    for (size_t t = 0; t < N; t++) {
+        reg = ((reg >> 1) | ((rng() & 1u) << 6)) & 127u;
+        o0[t] = __builtin_popcount(reg & 0171u) & 1u;
+        o1[t] = __builtin_popcount(reg & 0133u) & 1u;
+    }
+    std::vector<uint32_t> hh(N / 16 + 64, 0u);
+    std::uniform_real_distribution<double> U(0.0, 1.0);
+    for (size_t t = 0; t < N; t++) {
+        uint32_t a = o0[t] ^ (U(rng) < 0.04), b = o1[t] ^ (U(rng) < 0.04);
+        hh[t / 16] |= (a << (31 - 2 * (t % 16))) | (b << (30 - 2 * (t % 16)));
+    }
+    const double sigma = std::sqrt(1.0 / (2.0 * 0.5 * std::pow(10.0, 0.2)));
+    std::normal_distribution<double> G(0.0, sigma);
+    auto q8 = [&](double x) { long v = std::lround(x * 40.0); v = std::min(127L, std::max(-128L, v)); return (uint32_t)(uint8_t)(int8_t)v; };
+    std::vector<uint32_t> hs(N / 2 + 64, 0u);
+    for (size_t t = 0; t < N; t++) {
+        const uint32_t s0 = q8((o0[t] ? -1.0 : 1.0) + G(rng)), s1 = q8((o1[t] ? -1.0 : 1.0) + G(rng));
+        hs[t / 2] |= ((s0 << 8) | s1) << (16 * ((t % 2) ^ 1));
+    }
+    vd::Geom g;
+    g.packNum = (N - 64) / 32;
+    g.nchunks = 6400;
+    g.availStages = N;
+    g.scale = 1.0f;
+    CK(hipMalloc(&g.fair, vd::kFairBoardWords * 4));
+    CK(hipMemset(g.fair, 0xFF, vd::kFairBoardWords * 4));
+    const size_t strH = (hh.size() * 4 + 255) / 256 * 256, strS = (hs.size() * 4 + 255) / 256 * 256;
+    const size_t ostr = (g.packNum * 4 + 255) / 256 * 256;
+    char *bH, *bS, *bO;
+    CK(hipMalloc(&bH, strH * K));
+    CK(hipMalloc(&bS, strS * K));
+    CK(hipMalloc(&bO, ostr * K));
+    for (int k = 0; k < K; k++) {
+        CK(hipMemcpy(bH + k * strH, hh.data(), hh.size() * 4, hipMemcpyHostToDevice));
+        CK(hipMemcpy(bS + k * strS, hs.data(), hs.size() * 4, hipMemcpyHostToDevice));
+    }
+    vd::Geom gb = g;
+    gb.nbatch = (uint32_t)K;
+    gb.outStride = ostr;
+    const unsigned grid = 800u * (unsigned)K;  // two chunks per wave, 4 waves per workgroup
+    printf("TBS: 8 waves %d, 7 waves %d, 6 waves %d (SOFT8 layout %d %d %d)\n", vd::PkLds<8>::TBS, vd::PkLds<7>::TBS, vd::PkLds<6>::TBS,
+           vd::PkLds<8, true>::TBS, vd::PkLds<7, true>::TBS, vd::PkLds<6, true>::TBS);
+    const Variant vs[] = {VD_PKAB_VARIANTS};
+    const int nv = sizeof(vs) / sizeof(vs[0]);
+    hipEvent_t ev[3];
+    for (auto& evi : ev) CK(hipEventCreate(&evi));
+    std::vector<std::vector<float>> th(nv), ts(nv);
+    for (int r = 0; r < rounds + 1; r++)
+        for (int vi = 0; vi < nv; vi++) {
+            const int v = (vi + r) % nv;
+            vd::Geom gh = gb, gS = gb;
+            gh.inStride = strH;
+            gS.inStride = strS;
+            CK(hipEventRecord(ev[0]));
+            hipLaunchKernelGGL(vs[v].hard, dim3(grid), dim3(256), 0, 0, bH, bO, gh);
+            CK(hipEventRecord(ev[1]));
+            hipLaunchKernelGGL(vs[v].soft8, dim3(grid), dim3(256), 0, 0, bS, bO, gS);
+            CK(hipEventRecord(ev[2]));
+            CK(hipEventSynchronize(ev[2]));
+            float a, b;
+            CK(hipEventElapsedTime(&a, ev[0], ev[1]));
+            CK(hipEventElapsedTime(&b, ev[1], ev[2]));
+            if (r) { th[v].push_back(a / K); ts[v].push_back(b / K); }
+        }
+    std::vector<uint32_t> ref(g.packNum), got(g.packNum);
+    for (int w = 0; w < 2; w++)
+        for (int v = 0; v < nv; v++) {
+            if (v && !vs[v].exact) continue;
+            vd::Geom gg = gb;
+            gg.inStride = w ? strS : strH;
+            CK(hipMemset(bO, 0, ostr * K));
+            hipLaunchKernelGGL(w ? vs[v].soft8 : vs[v].hard, dim3(grid), dim3(256), 0, 0, w ? bS : bH, bO, gg);
+            CK(hipDeviceSynchronize());
+            CK(hipMemcpy(v ? got.data() : ref.data(), bO + (K - 1) * ostr, g.packNum * 4, hipMemcpyDeviceToHost));
+            if (v) {
+                size_t bad = 0;
+                for (size_t k = 0; k < ref.size(); k++) bad += ref[k] != got[k];
+                printf("exact twin %s %-40.40s: %zu words differ\n", w ? "soft8" : "hard ", vs[v].name, bad);
+            }
+        }
+    printf("%d rounds, %d batches per launch; ms per 32M-bit batch (median)\n", rounds, K);
+    printf("%-36s %9s %9s\n", "variant", "hard_b32", "soft8_b16");
+    for (int v = 0; v < nv; v++) printf("%-36.36s %9.4f %9.4f\n", vs[v].name, median(th[v]), median(ts[v]));
+    return 0;
+}
