@@ -1,7 +1,7 @@
 """bench.py's contract (host logic on CPU, the JSON line on the GPU).
 
-CPU: the roofline helpers read the committed round profiles (profiles/<PMC_ROUND>/pmc_summary.json and
-ablate.log) the way the bench line quotes them.  GPU: a short bench run prints one JSON line with the keys
+CPU: the roofline helpers read the committed round profiles (profiles/<PMC_ROUND>/pmc_summary.json,
+ablate_batched.log and valu_model.json) the way the bench line quotes them.  GPU: a short bench run prints one JSON line with the keys
 the driver and the judge read (metric, value, roofline with its binding VALU view, config)."""
 import json
 import os
@@ -23,10 +23,11 @@ def test_algorithmic_bytes_match_survey():
 
 
 def test_mix_ceiling_from_committed_ablation():
-    ms = bench.acs_only_ms("soft8_b16")
-    assert ms is not None and 0.05 < ms < 0.5, ms
-    # the packed kernels (batched HARD, SOFT4, FP32) have no ablation, so no ceiling
-    assert bench.acs_only_ms("hard_b32") is None and bench.acs_only_ms("fp32_f16") is None
+    # both headline kernels (vd_decode_pk) have their ACS-only ablation (tools/vd_pkab); the side configs none
+    for name in ("hard_b32", "soft8_b16"):
+        ms = bench.acs_only_ms(name)
+        assert ms is not None and 0.04 < ms < 0.2, (name, ms)
+    assert bench.acs_only_ms("fp32_f16") is None
 
 
 def test_valu_view_from_committed_pmc():
@@ -37,19 +38,20 @@ def test_valu_view_from_committed_pmc():
         # HBM bytes per launch within 1.2x of the algorithmic bytes
         alg = bench.algorithmic_bytes(0x00 if name == "hard_b32" else 0x12, 2 * bench.N_BITS)
         assert alg <= p["traffic_bytes"] <= 1.2 * alg, (name, p["traffic_bytes"], alg)
-        v = bench.valu_view(p, 0.18, 32_409_536, name, 31_999_936)
+        v = bench.valu_view(p, 0.11 if name == "hard_b32" else 0.13, 32_409_536, name, 31_999_936)
         for k in ("insts_per_chunk_stage", "issue_pct", "cycles_per_inst_per_simd", "pmc_run_clock_ghz",
-                  "issue_pct_live", "cycle_model_pct", "cycle_model_pct_live"):
+                  "issue_pct_live", "cycle_model_pct", "cycle_model_pct_live", "cycle_model", "mix_ceiling"):
             assert k in v, (name, k)
-        # the fp32 tagged kernel has its ACS-only ceiling; the packed HARD kernel none
-        assert ("mix_ceiling" in v) == (name == "soft8_b16")
         assert "busy_pct" not in v  # the gfx94x SIMD-16 formula does not read as a percentage on gfx950
-        # per chunk-stage: ~3.9 VALU instructions on vd_decode_tg, ~2 on vd_decode_pk (two chunks per wave)
-        lo, hi = (3.0, 5.0) if name == "soft8_b16" else (1.2, 3.0)
+        # per chunk-stage on vd_decode_pk (two chunks per wave): ~2.3 VALU instructions for HARD, ~3 for SOFT8
+        lo, hi = (2.5, 3.6) if name == "soft8_b16" else (1.8, 2.8)
         assert lo < v["insts_per_chunk_stage"] < hi, v["insts_per_chunk_stage"]
+        # the ISA-derived mix agrees with the counted instructions within 10 %
+        assert abs(v["cycle_model"]["valu_insts_per_chunk_stage_isa"] / v["insts_per_chunk_stage"] - 1) < 0.1, v
         assert 1.5 < v["pmc_run_clock_ghz"] < 2.6
-        # the cycle-weighted VALU model: the binding resource, well above the 2-cycle issue view
-        assert v["issue_pct"] < v["cycle_model_pct"] <= 100.0
+        # the per-opcode cycle model (ubench-priced ISA mix): the binding resource, above the 2-cycle issue view,
+        # and a fraction of the cycles available (a model above 100 % would contradict the timing)
+        assert v["issue_pct"] < v["cycle_model_pct"] <= 100.0 and v["cycle_model_pct_live"] <= 100.0, v
 
 
 @pytest.mark.gpu
