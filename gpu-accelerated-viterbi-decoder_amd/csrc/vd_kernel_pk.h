@@ -77,14 +77,15 @@ __device__ __forceinline__ void pk_stage_dpp(uint32_t& V, uint32_t m)
     else VD_PK_DPP("row_ror:8");
 #undef VD_PK_DPP
 }
-// LDS exchange, subtraction before the exchange (the partners share label and tag)
-template <bool X32>
+// LDS exchange, subtraction before the exchange (the partners share label and tag); SWZ: the ds_swizzle
+// bitmask-mode pattern of the lane xor (0x401F: xor 16), 0: ds_bpermute (xor 32)
+template <int SWZ>
 __device__ __forceinline__ void pk_stage_lds_pre(uint32_t& V, uint32_t m, int paddr)
 {
     uint32_t a, b;
     asm("v_sub_u32 %0, %1, %2" : "=v"(b) : "v"(V), "v"(m));
-    const uint32_t bp = X32 ? (uint32_t)__builtin_amdgcn_ds_bpermute(paddr, (int)b)
-                            : (uint32_t)__builtin_amdgcn_ds_swizzle((int)b, 0x401F);
+    const uint32_t bp = SWZ == 0 ? (uint32_t)__builtin_amdgcn_ds_bpermute(paddr, (int)b)
+                                 : (uint32_t)__builtin_amdgcn_ds_swizzle((int)b, SWZ);
     asm("v_add_u32 %0, %1, %2" : "=v"(a) : "v"(V), "v"(m));
     asm("v_pk_max_u16 %0, %1, %2" : "={v60}"(V) : "v"(a), "v"(bp));
 }
@@ -329,10 +330,12 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(SPL
             constexpr bool ODD = (r / 6) % 2 == 1;
             constexpr int RP = ODD ? r - 6 : r;
             const uint32_t m = (ABL & kAblNoTabReads) ? (uint32_t)aK[K] : ODD ? vp[RP].y : vp[RP].x;
+            // (the xor-8 and xor-7 stages through ds_swizzle too, 8 cycles of VALU instead of 10: +0.6 % / +5.5 %
+            // per HARD batch, the LDS pipe being the other busy resource: profiles/r05/abx_lds_exchanges.log)
             if constexpr (Q <= 3) pk_stage_dpp<Q>(V, m);
-            else if constexpr (Q == 4) pk_stage_lds_pre<false>(V, m, pa5);
+            else if constexpr (Q == 4) pk_stage_lds_pre<0x401F>(V, m, pa5);
             else if constexpr (ALT) pk_stage_lds_post(V, m, pa5);
-            else pk_stage_lds_pre<true>(V, m, pa5);
+            else pk_stage_lds_pre<0>(V, m, pa5);
             if constexpr (r + TGD < 96) issue(std::integral_constant<int, r + TGD>{});
             if constexpr (i % J == J - 1 && !(ABL & kAblNoReadout)) {
                 // field read-out, both chunks, then both fields cleared; renormalisation on the whole word
