@@ -112,9 +112,10 @@ struct PkFmt {
     static_assert(B == HARD || B == SOFT4 || B == SOFT8 || B == FP32, "int16 halves hold HARD, SOFT4, SOFT8 and FP32 metrics");
 };
 
-// LDS layout of a wave (words), for NW resident workgroups (waves per SIMD) per CU.  P2 (SOFT8): the ring
-// leads (its slots are 256-B aligned for the XOR addressing of the traceback): [ring | guard | table | guard |
-// guard], a slot = two words per position (fields 0..7 and 8..15; chunk A in the low, chunk B in the high half)
+// LDS layout of a wave (words), for NW resident workgroups (waves per SIMD) per CU.  RF (HARD, SOFT8): the
+// ring leads (its slots are 256-B aligned for the OR / XOR addressing of the tracebacks): [ring | guard | table
+// | guard | guard], a slot = two words per position (HARD: fields 0, 1 and 2, 3, chunk A in the even, chunk B
+// in the odd bytes; SOFT8: fields 0..7 and 8..15, chunk A in the low, chunk B in the high half)
 template <int NW = 8, bool P2 = false>
 struct PkLds {
     static constexpr int GW = kGuardWords;
@@ -133,7 +134,7 @@ struct PkLds {
 };
 static_assert(PkLds<8>::TBS == 5 && kWaves * PkLds<8>::WAVE * 4 <= 20480, "8 workgroups of 4 waves per CU");
 static_assert(PkLds<8, true>::TBS == 5 && kWaves * PkLds<8, true>::WAVE * 4 <= 20480 && PkLds<8, true>::WAVE % 64 == 0,
-              "SOFT8: 8 workgroups of 4 waves per CU, ring slots 256-B aligned");
+              "HARD, SOFT8: 8 workgroups of 4 waves per CU, ring slots 256-B aligned");
 
 // SOFT8 traceback of one word (header "Ring and traceback"): A = the lane's emit slot (block k + 1; the
 // convergence block k + 2 is the next slot, +512 B) | 2 for chunk B's half; z[r] = 2 + the position bit of the
@@ -172,6 +173,38 @@ __device__ __forceinline__ uint32_t pk2_traceback(uint32_t A, const uint32_t (&z
     return __builtin_bitreverse32(nat);  // word bit i <-> stage 63+32k-i
 }
 
+// HARD traceback of one word (header "HARD ring"): vd_decode_tg's field recursion (traceback_word_tg, J = 8) on
+// the ring-first layout.  base = the lane's emit slot | 1 for chunk B's bytes; sft[c] = tb_direct's off[c] - 2,
+// so (TX >> sft) & 0xFC is 4 times the position of the state (TX = T * 260: T in bits 2..7 and 8..13).
+template <int CORE>
+__device__ __forceinline__ uint32_t pk8_traceback(uint32_t base, const uint32_t (&sft)[3], const uint32_t (&m5)[3])
+{
+    constexpr bool FIX5 = CORE == B32;
+    uint32_t TX = 0, nat = 0;
+    // a field: the address by v_lshrrev + v_bitop3 ((t & 0xFC) | base), the byte by ds_read_u8 at a constant
+    // offset, Y = W ^ TX with the stride-6 fold Y ^= (Y >> 6) & 3 (v_xor, v_lshrrev, v_bitop3), M_B32's raw
+    // phase-0 bits back in (v_bitop3 select), the next TX = (Y & 63) * 260, the byte into nat (v_perm):
+    // 2-cycle ops but the multiply and the perm, where vd_decode_tg's form (v_bfe, v_lshl_add, v_bfe,
+    // v_bfi, v_lshl_or) takes 4 cycles each
+    auto step = [&](auto EMc, auto Gc) {
+        constexpr bool EM = decltype(EMc)::value;
+        constexpr int g = decltype(Gc)::value;
+        constexpr int BO = EM ? 0 : 2;
+        constexpr int c = (BO + 8 * g + 7) % 6;
+        constexpr int off = (EM ? 0 : 512) + 256 * (g / 2) + 2 * (g % 2);
+        const uint32_t A = __builtin_amdgcn_bitop3_b32(TX >> sft[c / 2], 0xFCu, base, 0xEA);
+        const uint32_t W = *(const __attribute__((address_space(3))) uint8_t*)(uintptr_t)(A + off);
+        uint32_t Y = W ^ TX;
+        Y = __builtin_amdgcn_bitop3_b32(Y, Y >> 6, 3u, 0x78);  // Y ^ ((Y >> 6) & 3)
+        if constexpr (FIX5) Y = __builtin_amdgcn_bitop3_b32(m5[((BO + 8 * g) % 6) / 2], W, Y, 0xCA);
+        if constexpr (!(EM && g == 0)) TX = __mul24(Y & 63u, 260u);
+        if constexpr (EM) nat = __builtin_amdgcn_perm(Y, nat, (0x03020100u & ~(0xFFu << (8 * g))) | (4u << (8 * g)));
+    };
+    sfor<4>([&](auto I) { step(std::false_type{}, std::integral_constant<int, 3 - decltype(I)::value>{}); });
+    sfor<4>([&](auto I) { step(std::true_type{}, std::integral_constant<int, 3 - decltype(I)::value>{}); });
+    return __builtin_bitreverse32(nat);  // word bit i <-> stage 63+32k-i
+}
+
 // Split single-batch launches (SPL).  A chunk of W words is cut into P parts at words cut(1) .. cut(P-1),
 // multiples of 3 blocks; part p emits words [cut(p), cut(p+1)).  Part 0 decodes from the chunk start (equal
 // metrics, as the chunk itself); part p >= 1 starts kPkWarm blocks before block cut(p) from equal metrics.
@@ -199,16 +232,17 @@ template <int CH, int CORE, int OB = 32, bool SPL = false, int NW = 8, int ABL =
 __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(SPL ? 7 : NW))) void vd_decode_pk(const void* __restrict__ in_all, void* __restrict__ out_all, Geom geo)
 {
     constexpr bool P2 = PkFmt<CH>::P2;
+    constexpr int J = PkFmt<CH>::J, S = PkFmt<CH>::S;
+    constexpr bool RF = P2 || J == 8;  // ring-first layout (PkLds)
     using IN = TgIn<CH>;
     using TT = TgTabLT<true>;
-    using LL = PkLds<NW, P2>;
-    constexpr int J = PkFmt<CH>::J, S = PkFmt<CH>::S;
+    using LL = PkLds<NW, RF>;
     constexpr bool ALT = CORE == B32;  // M_B32: the upper position half takes the +tag entries at phase 0
     __shared__ __attribute__((aligned(256))) uint32_t lds[kWaves * LL::WAVE];
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int pos = tg_pos(lane);
-    const int pp = ((pos << 1) | (pos >> 5)) & 63;  // P2: ring index p' = rotl6(p, 1)
+    const int ridx = P2 ? ((pos << 1) | (pos >> 5)) & 63 : pos;  // ring index (P2: p' = rotl6(p, 1))
     uint32_t* const wlds = lds + wv * LL::WAVE;
     char* const tabb = (char*)(wlds + LL::TAB_OFF);
     uint32_t* const ringA = wlds + LL::RING_OFF;
@@ -302,9 +336,9 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(SPL
     const char* const tbring = (const char*)(tbB ? ringB : ringA);
     const uint64_t tbStart = tbB ? crB.startWord : crA.startWord;
     const uint32_t tbWords = tbB ? crB.words : crA.words;
-    // P2: the lane's emit-slot LDS address without the slot index (chunk B: the high half of each word)
+    // RF: the lane's emit-slot LDS address (chunk B: the odd bytes / the high half of each word)
     const uint32_t tbA2 = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)(const char*)ringA +
-                          512u * tbl + (tbB ? 2u : 0u);
+                          512u * tbl + (tbB ? (P2 ? 2u : 1u) : 0u);
 
     typedef uint32_t u2v __attribute__((ext_vector_type(2)));
     typedef __attribute__((address_space(3))) const volatile u2v* lptr;
@@ -320,8 +354,10 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(SPL
         constexpr int PH = decltype(PHc)::value;
         constexpr int BB = PH / 2;
         uint32_t wA = 0, wB = 0;
-        uint32_t cw[4];  // J = 4: field-pair words; J = 2: the two ring words
+        uint32_t cw[4];  // J = 4: field-pair words; J = 2, 8: the two ring words
+        uint32_t xe;     // J = 8: the even field's take-bits
         (void)cw;
+        (void)xe;
         sfor<32>([&](auto I) {
             constexpr int i = decltype(I)::value;
             constexpr int K = (PH + i) % 6;
@@ -362,21 +398,26 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(SPL
                     if constexpr (h == 0) cw[g / 8] = x >> 1;
                     else asm("v_lshl_or_b32 %0, %1, %2, %0" : "+v"(cw[g / 8]) : "v"(x), "n"(2 * h - 1));
                 } else if constexpr (J == 8) {
-                    // bits 1..8 of each half into byte g of its ring word (SDWA)
-#define VD_PK_RO(SEL, UNUSED)                                                                                \
-    "v_lshrrev_b32_sdwa %[wa], 1, %[V] dst_sel:" SEL " dst_unused:" UNUSED " src0_sel:DWORD src1_sel:DWORD\n\t"  \
-    "v_lshrrev_b32_sdwa %[wb], 1, %[V] dst_sel:" SEL " dst_unused:" UNUSED " src0_sel:DWORD src1_sel:WORD_1\n\t" \
-    "v_bitop3_b32 %[V], %[V], %[fnm], %[fhf] bitop3:0xea"
-                    if constexpr (g == 0)
-                        asm(VD_PK_RO("BYTE_0", "UNUSED_PAD") : [V] "+{v60}"(V), [wa] "=&v"(wA), [wb] "=&v"(wB) : VD_PK_IN);
+                    // x = V >> 1: each half's take-bits (bits 1..8) in bytes 0 and 2; an odd field's x and the
+                    // even field's before it become ring word g / 2 = [B odd, A odd, B even, A even] by one
+                    // v_perm_b32 (2 + 2 + 2 cycles per field for both chunks, where two SDWA shifts took 8)
+#define VD_PK_RO8E "v_lshrrev_b32 %[x], 1, %[V]\n\tv_bitop3_b32 %[V], %[V], %[fnm], %[fhf] bitop3:0xea"
+#define VD_PK_RO8O                                                                                    \
+    "v_lshrrev_b32 %[t], 1, %[V]\n\tv_bitop3_b32 %[V], %[V], %[fnm], %[fhf] bitop3:0xea\n\t"           \
+    "v_perm_b32 %[c], %[t], %[x], %[sel]"
+                    uint32_t t;
+                    uint32_t& x8 = xe;  // (named: asm operands alone do not capture)
+                    uint32_t& c8 = cw[g / 2];
+                    if constexpr (g % 2 == 0)
+                        asm(VD_PK_RO8E : [V] "+{v60}"(V), [x] "=&v"(x8) : VD_PK_IN);
                     else if constexpr (g == 1)
-                        asm(VD_PK_RO("BYTE_1", "UNUSED_PRESERVE") : [V] "+{v60}"(V), [wa] "+v"(wA), [wb] "+v"(wB) : VD_PK_IN);
-                    else if constexpr (g == 2)
-                        asm(VD_PK_RO("BYTE_2", "UNUSED_PRESERVE") : [V] "+{v60}"(V), [wa] "+v"(wA), [wb] "+v"(wB) : VD_PK_IN);
+                        asm(VD_PK_RO8O : [V] "+{v60}"(V), [t] "=&v"(t), [c] "=v"(c8) : [x] "v"(x8), [sel] "s"(0x06040200u), VD_PK_IN);
                     else
-                        asm(VD_PK_RO("BYTE_3", "UNUSED_PRESERVE") VD_PK_RN
-                            : [V] "+{v60}"(V), [wa] "+v"(wA), [wb] "+v"(wB), [sr] "=&s"(sr) : VD_PK_IN : "scc");
-#undef VD_PK_RO
+                        asm(VD_PK_RO8O VD_PK_RN
+                            : [V] "+{v60}"(V), [t] "=&v"(t), [c] "=v"(c8), [sr] "=&s"(sr)
+                            : [x] "v"(x8), [sel] "s"(0x06040200u), VD_PK_IN : "scc");
+#undef VD_PK_RO8E
+#undef VD_PK_RO8O
                 } else {
                     // bits 1..4 of each half: the even field's as V >> 1, the odd field's (V << 3) into the
                     // high nibbles of the pair word (chunk A byte 0, chunk B byte 2)
@@ -406,6 +447,10 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(SPL
             wA = __builtin_amdgcn_perm(p23, p01, 0x05040100u);
             wB = __builtin_amdgcn_perm(p23, p01, 0x07060302u);
         }
+        if constexpr (J == 8) {
+            wA = cw[0];
+            wB = cw[1];
+        }
         if constexpr (J == 2) {
             // the ring words are cw[0], cw[1]; M_B32: complement the upper half's phase-0 bits (fields g with
             // (PH + 2g) % 6 == 0: bit 0 of their pair, both chunks)
@@ -430,9 +475,9 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(SPL
         }
         wave_sync();
         if (j >= 1) {
-            if constexpr (P2) {
-                ringA[(j - 1 - kb) * 128 + pp] = wA;
-                ringA[(j - 1 - kb) * 128 + 64 + pp] = wB;
+            if constexpr (RF) {
+                ringA[(j - 1 - kb) * 128 + ridx] = wA;
+                ringA[(j - 1 - kb) * 128 + 64 + ridx] = wB;
             } else {
                 ringA[(j - 1 - kb) * 64 + pos] = wA;
                 ringB[(j - 1 - kb) * 64 + pos] = wB;
@@ -454,6 +499,11 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(SPL
                     const uint32_t mlo = rho == 0u ? 0xFFFFFFFCu : rho == 2u ? 0x3CF3CF3Cu : 0x0C30C30Cu;
                     const uint32_t zm[3] = {3u << z[0], 3u << z[1], 3u << z[2]};
                     w = pk2_traceback<CORE>(tbA2, z, zm, rho, mlo);
+                } else if constexpr (J == 8) {
+                    const TbC tc = tb_direct<8, CORE == B32>((int)k);
+                    const uint32_t sft[3] = {tc.off[0] - 2u, tc.off[1] - 2u, tc.off[2] - 2u};
+                    const uint32_t m5[3] = {tc.m50, tc.m50 >> 2, tc.m50 >> 4};
+                    w = pk8_traceback<CORE>(tbA2, sft, m5);
                 } else {
                     const TbC tc = tb_direct<(J < 6 ? 6 : J), CORE == B32>((int)k);
                     w = traceback_word_tg<J, CORE == B32>(tbring, (tbl + 1u) * 256u, tc);
@@ -470,9 +520,9 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(SPL
                 }
             }
             wave_sync();
-            if constexpr (P2) {  // block j becomes slot 0 of the next batch
-                ringA[pp] = wA;
-                ringA[64 + pp] = wB;
+            if constexpr (RF) {  // block j becomes slot 0 of the next batch
+                ringA[ridx] = wA;
+                ringA[64 + ridx] = wB;
             } else {
                 ringA[pos] = wA;
                 ringB[pos] = wB;
@@ -485,15 +535,44 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(SPL
     // the four entries of a stage for both chunks: E[L] = BM[L] * 2^S + tg0 per half (TgFmt::INT's table),
     // from (A, B) = (BM[3], BM[2]) of each chunk packed as A_A + A_B * 2^16 (signed halves; |.| <= 16 except
     // SOFT8's 256: its entries by shifts, since BM_B * 2^16 leaves __mul24's 24 bits)
+    // HARD / SOFT8 words (not the fused-LLR formats): both chunks' inputs merged into one word by v_perm_b32,
+    // then (A, B) of both chunks at once in non-negative halves (PK8 below)
+    constexpr bool PK8 = CH == HARD || CH == SOFT8;
+    // HARD: the 16-bit half of the input word holding the lane's stage (li % 16 < 8: the high half) and the
+    // shift that brings its two bits (r0, r1) to bits 1, 0
+    const uint32_t hselA = (sA & 15) < 8 ? 0x07060302u : 0x05040100u, hselB = (sB & 15) < 8 ? 0x07060302u : 0x05040100u;
+    const uint32_t hshA = 14u - 2u * (uint32_t)(sA & 7), hshB = 14u - 2u * (uint32_t)(sB & 7);
     auto put_row = [&](auto PT, typename IN::raw_t wa, typename IN::raw_t wb, int li, int K) {
         constexpr int part = decltype(PT)::value;
         const int32_t tg = part ? tg0B : tg0A;
+        auto f = [](int32_t x) { return __builtin_bit_cast(float, x); };
+        int32_t e0, e1, e2, e3;
+        if constexpr (CH == HARD) {
+            // t: chunk A's (r0, r1) at bits 1, 0, chunk B's at 17, 16; A = r0 + r1 - 1, B = r0 - r1 per half,
+            // entries E3 = A 2^9 + tg, E2 = B 2^9 + tg, E0 = 2 tg - E3, E1 = 2 tg - E2 (both chunks: the halves
+            // R0, R1 are non-negative, so the 32-bit sums are the packed values m = EB 2^16 + EA)
+            const uint32_t t = __builtin_amdgcn_perm(wb, wa, part ? hselB : hselA) >> (part ? hshB : hshA);
+            const uint32_t R0 = (t >> 1) & 0x10001u, R1 = t & 0x10001u;
+            e3 = (int32_t)(((R0 + R1) << 9) + (uint32_t)tg - 0x02000200u);
+            e2 = (int32_t)(((R0 - R1) << 9) + (uint32_t)tg);
+            e0 = 2 * tg - e3;
+            e1 = 2 * tg - e2;
+        } else if constexpr (CH == SOFT8) {
+            // X = [s0B, s1B, s0A, s1A] (bytes 3..0); U0, U1 = s0 + 128, s1 + 128 per half (v_bitop3 (x &
+            // 0x00FF00FF) ^ 0x00800080): A = U0 + U1 - 256, B = U0 - U1
+            const uint32_t X = __builtin_amdgcn_perm(wb, wa, 0x05040100u);
+            const uint32_t U1 = __builtin_amdgcn_bitop3_b32(X, 0x00FF00FFu, 0x00800080u, 0x6A);
+            const uint32_t U0 = __builtin_amdgcn_bitop3_b32(X >> 8, 0x00FF00FFu, 0x00800080u, 0x6A);
+            e3 = (int32_t)(((U0 + U1) << S) + (uint32_t)tg - 0x08000800u);
+            e2 = (int32_t)(((U0 - U1) << S) + (uint32_t)tg);
+            e0 = 2 * tg - e3;
+            e1 = 2 * tg - e2;
+        }
+        if constexpr (!PK8) {
         int AA, BA, AB, BBv;
         IN::ab(wa, li, AA, BA, geo.scale);
         IN::ab(wb, li, AB, BBv, geo.scale);
         const int32_t pa = AA + AB * 65536, pb = BA + BBv * 65536;
-        auto f = [](int32_t x) { return __builtin_bit_cast(float, x); };
-        int32_t e0, e1, e2, e3;
         if constexpr (P2) {
             e3 = (int32_t)((uint32_t)pa << S) + tg;
             e2 = (int32_t)((uint32_t)pb << S) + tg;
@@ -504,6 +583,7 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(SPL
             e2 = __mul24(pb, 1 << S) + tg;
             e0 = __mul24(pa, -(1 << S)) + tg;
             e1 = __mul24(pb, -(1 << S)) + tg;
+        }
         }
         lds_write_addtid4<256 * part, TT::REGION>(tabl, f(e0), f(e1), f(e2), f(e3));
         if (ALT && K == 0) {  // phase-0 lanes: the +tag entries E+[L] = BM[L] * 2^S - tg0 (ALT area)
