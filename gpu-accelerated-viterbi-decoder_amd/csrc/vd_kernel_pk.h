@@ -339,6 +339,15 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(SPL
     // RF: the lane's emit-slot LDS address (chunk B: the odd bytes / the high half of each word)
     const uint32_t tbA2 = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)(const char*)ringA +
                           512u * tbl + (tbB ? (P2 ? 2u : 1u) : 0u);
+    // RF: the lane's phase constants for kb = 0 in bytes 0..2 of two words; a pass rotates them by kb % 3 (one
+    // v_perm_b32 each with a wave-uniform selector) instead of deriving them from k % 3 per lane.
+    //  HARD, q = (k + 1) % 3 (tb_direct): sft = off - 2 = (5, 3, 1) and M_B32's phase-0 masks (0x41, 0x10, 0x04)
+    //  (low bytes of m50 >> 0, 2, 4), rotated left by q;  SOFT8, u = (k + 2) % 3: z = (2, 4, 6) rotated left by u
+    auto rot3 = [](uint32_t w, uint32_t r) {
+        return __builtin_amdgcn_perm(w, w, r == 0u ? 0x03020100u : r == 1u ? 0x03000201u : 0x03010002u);
+    };
+    const uint32_t q0 = (tbl + (P2 ? 2u : 1u)) % 3u;
+    const uint32_t phA = rot3(P2 ? 0x00060402u : 0x00010305u, q0), phB = P2 ? 0u : rot3(0x00041041u, q0);
 
     typedef uint32_t u2v __attribute__((ext_vector_type(2)));
     typedef __attribute__((address_space(3))) const volatile u2v* lptr;
@@ -489,20 +498,23 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(SPL
             const uint32_t k = kb + tbl;
             if (!(ABL & kAblNoTraceback) && tbl < nw && k >= (tbB ? kminB : kminA) && k < (tbB ? kmaxB : kmaxA)) {
                 uint32_t w;
+                const uint32_t r3 = kb % 3u;  // wave-uniform
+                const uint32_t PA = rot3(phA, r3);
                 if constexpr (P2) {
                     // the stage phase of the convergence block k + 2: field g of it starts at position bit
-                    // 2 ((k + 2 + g) % 3)
-                    const uint32_t u = (k + 2u) % 3u;
-                    const uint32_t z[3] = {2u * u + 2u, u == 2u ? 2u : 2u * u + 4u, u == 0u ? 6u : 2u * u};
-                    // emit snapshots: rotate each 6-bit group right by 2u (pk2_traceback)
-                    const uint32_t rho = 2u * u;
-                    const uint32_t mlo = rho == 0u ? 0xFFFFFFFCu : rho == 2u ? 0x3CF3CF3Cu : 0x0C30C30Cu;
+                    // 2 ((k + 2 + g) % 3); z[i]: bytes of PA (the shifts read bits 4..0 of their operand), zm =
+                    // 3 << z; the emit snapshots are rotated right by rho = 2u per 6-bit group (pk2_traceback),
+                    // mlo = their low 6 - rho bits: 0x04104104 (2^(6 - rho) - 1)
+                    const uint32_t z[3] = {PA, PA >> 8, PA >> 16};
                     const uint32_t zm[3] = {3u << z[0], 3u << z[1], 3u << z[2]};
+                    const uint32_t rho = (PA & 0xFFu) - 2u;
+                    const uint32_t mlo = (0x04104104u << (6u - rho)) - 0x04104104u;
                     w = pk2_traceback<CORE>(tbA2, z, zm, rho, mlo);
                 } else if constexpr (J == 8) {
-                    const TbC tc = tb_direct<8, CORE == B32>((int)k);
-                    const uint32_t sft[3] = {tc.off[0] - 2u, tc.off[1] - 2u, tc.off[2] - 2u};
-                    const uint32_t m5[3] = {tc.m50, tc.m50 >> 2, tc.m50 >> 4};
+                    // sft[i], m5[i]: bytes of PA, PB (the shifts read bits 4..0; M_B32's select only bits 7..0)
+                    const uint32_t PB = rot3(phB, r3);
+                    const uint32_t sft[3] = {PA, PA >> 8, PA >> 16};
+                    const uint32_t m5[3] = {PB, PB >> 8, PB >> 16};
                     w = pk8_traceback<CORE>(tbA2, sft, m5);
                 } else {
                     const TbC tc = tb_direct<(J < 6 ? 6 : J), CORE == B32>((int)k);
