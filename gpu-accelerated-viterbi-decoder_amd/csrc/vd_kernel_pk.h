@@ -5,11 +5,12 @@
 // int16x2 idea of selfPM/pairPM<M_B16>, viterbiACS.cuh:113-119,216-220).
 //
 // Why it is exact.  A HARD metric needs few bits: every path metric lies within D = 12 units of the best
-// one and the best grows by at most 1 unit per stage, so between two renormalisations (32 stages) the
-// candidates of a stage stay within [-14, +47] units of the reference (vd_kernel_tg.h "Range").  With the
+// one and the best grows by at most 1 unit per stage, so R stages after a renormalisation the candidates of
+// a stage stay within [-14, D + R + 2] units of position 0's metric (vd_kernel_tg.h "Range").  With the
 // tagged scheme of the int32 patterns (TgFmt::INT: V = BASE + metric * 2^9 + 2^8 + h, 8-stage history
-// fields, |h| < 2^8) every value a stage computes lies in BASE + [-14 * 512, 48 * 512): with BASE = 16384,
-// in [9216, 40960), inside an unsigned 16-bit half.  Two chunks' metrics VA, VB sit in one 32-bit word
+// fields, |h| < 2^8) and one renormalisation per 96-stage group (R = 96: [-14, 110] units) every value a
+// stage computes lies in BASE + [-14 * 512, 111 * 512): with BASE = 7680, in [512, 64512), inside an
+// unsigned 16-bit half.  Two chunks' metrics VA, VB sit in one 32-bit word
 // V = VB * 2^16 + VA, and a table entry holds both chunks' entries as m = EB * 2^16 + EA (signed halves).
 // 32-bit integer addition is a ring homomorphism: V + m = (VB + EB) * 2^16 + (VA + EA) exactly, and the
 // word's halves ARE VA + EA and VB + EB whenever both lie in [0, 2^16) -- which the bound guarantees for
@@ -107,8 +108,8 @@ struct PkFmt {
     static constexpr bool P2 = B == SOFT8;  // 2-stage fields, position-space ring (header)
     static constexpr int J = B == HARD ? 8 : P2 ? 2 : 4;
     static constexpr int S = J + 1;
-    static constexpr uint32_t BASE = B == HARD ? 16384u : P2 ? 25600u : 8192u;
-    static constexpr int RN = P2 ? 8 : 32;
+    static constexpr uint32_t BASE = B == HARD ? 7680u : P2 ? 25600u : 8192u;
+    static constexpr int RN = B == HARD ? 96 : P2 ? 8 : 32;
     static_assert(B == HARD || B == SOFT4 || B == SOFT8 || B == FP32, "int16 halves hold HARD, SOFT4, SOFT8 and FP32 metrics");
 };
 
@@ -377,7 +378,7 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(SPL
             const uint32_t m = (ABL & kAblNoTabReads) ? (uint32_t)aK[K] : ODD ? vp[RP].y : vp[RP].x;
             // (the xor-8 and xor-7 stages through ds_swizzle too, 8 cycles of VALU instead of 10: +0.6 % / +5.5 %
             // per HARD batch, the LDS pipe being the other busy resource: profiles/r05/abx_lds_exchanges.log)
-            if constexpr (Q <= 3) pk_stage_dpp<Q>(V, m);
+            if constexpr (Q <= 3 || (ABL & kAblNoLdsX)) pk_stage_dpp<(Q <= 3 ? Q : 0)>(V, m);
             else if constexpr (Q == 4) pk_stage_lds_pre<0x401F>(V, m, pa5);
             else if constexpr (ALT) pk_stage_lds_post(V, m, pa5);
             else pk_stage_lds_pre<0>(V, m, pa5);
@@ -420,6 +421,8 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(SPL
                     if constexpr (g % 2 == 0)
                         asm(VD_PK_RO8E : [V] "+{v60}"(V), [x] "=&v"(x8) : VD_PK_IN);
                     else if constexpr (g == 1)
+                        asm(VD_PK_RO8O : [V] "+{v60}"(V), [t] "=&v"(t), [c] "=v"(c8) : [x] "v"(x8), [sel] "s"(0x06040200u), VD_PK_IN);
+                    else if constexpr (PH != 4)  // (RN = 96: the renormalisation ends the group's last block)
                         asm(VD_PK_RO8O : [V] "+{v60}"(V), [t] "=&v"(t), [c] "=v"(c8) : [x] "v"(x8), [sel] "s"(0x06040200u), VD_PK_IN);
                     else
                         asm(VD_PK_RO8O VD_PK_RN

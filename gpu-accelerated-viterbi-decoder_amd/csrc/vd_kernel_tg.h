@@ -59,6 +59,7 @@ constexpr int kAblNoStores = 524288;
 // vd_decode_pk study: input loads two groups ahead (a second register set) instead of one
 constexpr int kAblLoad2 = 1048576;
 constexpr int kAblAcsOnly = kAblNoTraceback | kAblNoTabReads | kAblNoReadout | kAblNoTabBuild | kAblNoLoads;
+constexpr int kAblNoLdsX = 2097152;  // vd_decode_pk: the two LDS-exchange stages as DPP stages (wrong outputs)
 
 template <int CH>
 struct TgFmt {

@@ -163,7 +163,7 @@ def scc_reads_after_renorm(asm):
         for k, l in enumerate(body):
             # the VBASE subtraction: s_sub_u32 s, s, VBASE (tg, pk HARD / SOFT4 / FP32), or s_sub_u32 s, K, s with
             # K = VBASE - 0x10001 (pk SOFT8's merged clear + renormalisation)
-            if not (l.startswith("s_sub_u32") and re.search(r"(, (0x4b2\w+|0x41004100|0x20102010|0x100|0x10000|256|65536)$|"
+            if not (l.startswith("s_sub_u32") and re.search(r"(, (0x4b2\w+|0x1f001f00|0x20102010|0x100|0x10000|256|65536)$|"
                                                             r"^s_sub_u32 s\d+, 0x64036403, s\d+$)", l)):
                 continue
             for l2 in body[k + 1:k + 60]:

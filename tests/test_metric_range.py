@@ -115,3 +115,38 @@ def test_bounds_fit_the_binade():
     # 40 stages would not fit SOFT8
     bm_max, S = 256, 9
     assert (6 * 512 + 40 * bm_max + bm_max + 2) * 2 ** S >= above
+
+
+@pytest.mark.parametrize("name,bm_max,D,S,R,base", [
+    ("HARD", 1, 12, 9, 96, 7680),     # 8-stage fields, one renormalisation per 96-stage group
+    ("SOFT4", 16, 192, 5, 32, 8192),  # 4-stage fields (FP32 the same: BMmax 16)
+    ("SOFT8", 256, 2816, 3, 8, 25600),  # 2-stage fields, D = 11 * 256 (vd_kernel_pk.h "SOFT8 range")
+])
+def test_packed_halves_fit(name, bm_max, D, S, R, base):
+    """vd_kernel_pk.h PkFmt: the metric part of a candidate is a previous metric (within [-D, D + (R-1) BMmax]
+    of position 0's at the last renormalisation: properties 1-3) plus a branch metric, so within
+    [-(D + BMmax), D + R * BMmax] units of 2^S around the half's base; the history field (tags included)
+    adds [0, 2^S).  The whole range lies inside an unsigned 16-bit half, so the 32-bit adds of the two halves
+    never carry or borrow across them."""
+    lo = base - (D + bm_max) * 2 ** S
+    hi = base + (D + R * bm_max) * 2 ** S + 2 ** S - 1
+    assert 0 <= lo and hi < 2 ** 16, (name, lo, hi)
+    # one more group (HARD) / period (SOFT8) between renormalisations would not fit
+    if name != "SOFT4":
+        R2 = R + (96 if name == "HARD" else 8)
+        assert base + (D + R2 * bm_max) * 2 ** S + 2 ** S - 1 >= 2 ** 16
+
+
+def test_soft8_spread_bound():
+    """D = 2816 for SOFT8: the largest spread seen over saturated codewords and random full-range inputs
+    stays within 11 * 256 (vd_kernel_pk.h "SOFT8 range"; the generic (K-1)(BMmax-BMmin) would be 3072)."""
+    rng = np.random.default_rng(5)
+    worst = 0
+    for _ in range(4):
+        s = rng.integers(-128, 128, (2000, 2))
+        hist, _ = _forward(s[:, 0], s[:, 1])
+        worst = max(worst, int((hist.max(axis=1) - hist.min(axis=1)).max()))
+        c = _encode(rng.integers(0, 2, 2000))
+        hist, _ = _forward(np.where(c[:, 0] == 1, -128, 127), np.where(c[:, 1] == 1, -128, 127))
+        worst = max(worst, int((hist.max(axis=1) - hist.min(axis=1)).max()))
+    assert worst <= 11 * 256, worst

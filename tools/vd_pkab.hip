@@ -27,6 +27,9 @@ struct Variant { const char* name; KFn hard, soft8; bool exact; };
     {"-table build (ablation)", pk<vd::HARD, vd::B32, vd::kAblNoTabBuild>(), pk<vd::SOFT8, vd::B16, vd::kAblNoTabBuild>(), false}, \
     {"-table reads (ablation)", pk<vd::HARD, vd::B32, vd::kAblNoTabReads>(), pk<vd::SOFT8, vd::B16, vd::kAblNoTabReads>(), false}, \
     {"-input loads (ablation)", pk<vd::HARD, vd::B32, vd::kAblNoLoads>(), pk<vd::SOFT8, vd::B16, vd::kAblNoLoads>(), false}, \
+    {"LDS exchanges as DPP (ablation)", pk<vd::HARD, vd::B32, vd::kAblNoLdsX>(), pk<vd::SOFT8, vd::B16, vd::kAblNoLdsX>(), false}, \
+    {"ACS only, LDS exchanges as DPP", pk<vd::HARD, vd::B32, vd::kAblAcsOnly | vd::kAblNoLdsX>(),                       \
+     pk<vd::SOFT8, vd::B16, vd::kAblAcsOnly | vd::kAblNoLdsX>(), false},                                                 \
     {"7 waves/SIMD, 6 words per traceback", pk<vd::HARD, vd::B32, 0, 7>(), pk<vd::SOFT8, vd::B16, 0, 7>(), true},      \
     {"6 waves/SIMD, 8 words per traceback", pk<vd::HARD, vd::B32, 0, 6>(), pk<vd::SOFT8, vd::B16, 0, 6>(), true},
 #endif
