@@ -441,10 +441,12 @@ def single_launch_side_measurement(batches, stream, sptr, reps=20, keep=None):
                        for k in range(n)]
         settle(run)
         e = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+        rd0 = vitdec.split_redecodes(b["inps"].device.index or 0)
         e[0].record(stream)
         run()
         e[1].record(stream)
         torch.cuda.synchronize()
+        redec = vitdec.split_redecodes(b["inps"].device.index or 0) - rd0
         ms = e[0].elapsed_time(e[1]) / n
         nout = b["nout"]
         # every segment-launch output equals the batched launch's output of the same batch (word for word,
@@ -453,6 +455,7 @@ def single_launch_side_measurement(batches, stream, sptr, reps=20, keep=None):
                 for k in range(n)]
         res[b["name"]] = {"kernel": b["dec"].kernel_for(b["input_num"], 1, b["llr"]), "kernel_ms": round(ms, 4),
                           "gbps": round(b["msg"] / (ms * 1e-3) / 1e9, 2), "launches": n,
+                          "split_redecodes_per_launch": round(redec / n, 2),
                           "equals_batched_launch": f"{sum(same)} of {n} batches"}
         if keep is not None:
             keep.append((f"single_launch.{b['name']}[batch 0]", b["opt"], b["inp"].cpu().numpy(),

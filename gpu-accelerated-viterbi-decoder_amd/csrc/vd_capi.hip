@@ -146,9 +146,8 @@ launch_fn pick_pk_ch(int o)
     // (the speculative second part rarely converges on saturated random values: 0.36 against 0.19 ms), and on
     // codewords it measured no faster than vd_decode_tg's segment launch (0.182 against 0.181 ms)
     case 2:
-        if constexpr (SPL) return nullptr;
-        else return out_of(o) == 1 ? (met_of(o) == 0 ? &launch_pk<L + vd::SOFT8, 0, 16, false> : &launch_pk<L + vd::SOFT8, 1, 16, false>)
-                                   : (met_of(o) == 0 ? &launch_pk<L + vd::SOFT8, 0, 32, false> : &launch_pk<L + vd::SOFT8, 1, 32, false>);
+        return out_of(o) == 1 ? (met_of(o) == 0 ? &launch_pk<L + vd::SOFT8, 0, 16, SPL> : &launch_pk<L + vd::SOFT8, 1, 16, SPL>)
+                              : (met_of(o) == 0 ? &launch_pk<L + vd::SOFT8, 0, 32, SPL> : &launch_pk<L + vd::SOFT8, 1, 32, SPL>);
     case 4: return pick_pk_ob<L + vd::FP32, SPL>(o);
     }
     return nullptr;
@@ -244,7 +243,7 @@ struct vd_decoder {
     DeviceState* ds = nullptr;  // the device's board / segment tables (looked up once, vd_create)
     int split = 1;              // segment launches: 0 none (VD_NO_SPLIT=1), 1 pieces, 2 thirds, 3 sevenths (VD_SPLIT=...)
     int pk = 1;                 // HARD/SOFT4/FP32 launches on vd_decode_pk (VD_NO_PK=1: on vd_decode_tg)
-    int pksplit = 1;            // their single-batch launches split on vd_decode_pk (VD_PK_SPLIT=0: tg segments)
+    int pksplit = 1;            // their single-batch launches split on vd_decode_pk (VD_PK_SPLIT=0: tg segments; 2: SOFT8 too)
     int pktail = 1;             // ... with the tail chunks in 4-wave workgroups (VD_PK_TAIL=0: one chunk per wave)
     uint32_t* check = nullptr;  // LDS guard violation counter (vd_set_guard_check), null = off
 };
@@ -342,7 +341,7 @@ static Form plan_form(const vd_decoder* d, uint64_t packNum, uint32_t nbatch, bo
     const uint64_t w32 = out_of(options) != 0 ? packNum / 2 : packNum;
     const bool splitok = nbatch == 1 && d->pk && d->pksplit && d->split && vd::kChunks % vd::kWaves == 0 &&
                          w32 / vd::kChunks >= (uint64_t)vd::kSplitMinWords;
-    if (splitok && pick_pk<true>(options, llr)) return Form::PkSplit;
+    if (splitok && (ch_of(options) != 2 || d->pksplit == 2) && pick_pk<true>(options, llr)) return Form::PkSplit;
     return Form::Tg;
 }
 
@@ -477,7 +476,7 @@ int vd_create(int options, size_t preallocInputNum, int device, vd_decoder** out
     const char* nopk = std::getenv("VD_NO_PK");
     d->pk = nopk && nopk[0] == '1' ? 0 : 1;
     const char* pks = std::getenv("VD_PK_SPLIT");
-    d->pksplit = pks && pks[0] == '0' ? 0 : 1;
+    d->pksplit = pks && pks[0] == '0' ? 0 : pks && pks[0] == '2' ? 2 : 1;
     const char* pkt = std::getenv("VD_PK_TAIL");
     d->pktail = pkt && pkt[0] == '0' ? 0 : 1;
     const char* chk = std::getenv("VD_CHECK");
