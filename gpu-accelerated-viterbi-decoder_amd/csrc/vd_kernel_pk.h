@@ -113,29 +113,24 @@ struct PkFmt {
     static_assert(B == HARD || B == SOFT4 || B == SOFT8 || B == FP32, "int16 halves hold HARD, SOFT4, SOFT8 and FP32 metrics");
 };
 
-// LDS layout of a wave (words), for NW resident workgroups (waves per SIMD) per CU.  RF (HARD, SOFT8): the
-// ring leads (its slots are 256-B aligned for the OR / XOR addressing of the tracebacks): [ring | guard | table
-// | guard | guard], a slot = two words per position (HARD: fields 0, 1 and 2, 3, chunk A in the even, chunk B
-// in the odd bytes; SOFT8: fields 0..7 and 8..15, chunk A in the low, chunk B in the high half)
-template <int NW = 8, bool P2 = false>
+// LDS layout of a wave (words), for NW resident workgroups (waves per SIMD) per CU.  The ring leads (its slots
+// are 256-B aligned for the OR / XOR addressing of the tracebacks): [ring | guard | table | guard | guard], a
+// slot = two words per position (HARD: fields 0, 1 and 2, 3, chunk A in the even, chunk B in the odd bytes;
+// SOFT8: fields 0..7 and 8..15, chunk A in the low, chunk B in the high half; SOFT4 / FP32: chunk A's nibbles
+// of fields 0..7, then chunk B's, 256 B apart)
+template <int NW = 8>
 struct PkLds {
     static constexpr int GW = kGuardWords;
     static constexpr int TAB = TgTabLT<true>::BYTES / 4;
     static constexpr int LDSW = 163840 / 4 / (NW * kWaves);                // a wave's share
     static constexpr int TBS = (LDSW - 3 * GW - TAB) / 128 - 1;            // words per traceback batch and chunk
-    static constexpr int RING = (TBS + 1) * 64;                            // words per chunk ring
-    static constexpr int TAB_OFF = P2 ? 2 * RING + GW : GW, RING_OFF = P2 ? 0 : 2 * GW + TAB;
-    static constexpr int WAVE0 = 3 * GW + TAB + 2 * RING;
-    static constexpr int WAVE = P2 ? (WAVE0 + 63) / 64 * 64 : WAVE0;
-    static __device__ __forceinline__ int guard(int i)
-    {
-        if constexpr (P2) return 2 * RING + (i < GW ? i : TAB + i);
-        return i < GW ? i : i < 2 * GW ? TAB + i : TAB + 2 * RING + i;
-    }
+    static constexpr int RING = (TBS + 1) * 64;                            // words per chunk
+    static constexpr int TAB_OFF = 2 * RING + GW, RING_OFF = 0;
+    static constexpr int WAVE = (3 * GW + TAB + 2 * RING + 63) / 64 * 64;
+    static __device__ __forceinline__ int guard(int i) { return 2 * RING + (i < GW ? i : TAB + i); }
 };
-static_assert(PkLds<8>::TBS == 5 && kWaves * PkLds<8>::WAVE * 4 <= 20480, "8 workgroups of 4 waves per CU");
-static_assert(PkLds<8, true>::TBS == 5 && kWaves * PkLds<8, true>::WAVE * 4 <= 20480 && PkLds<8, true>::WAVE % 64 == 0,
-              "HARD, SOFT8: 8 workgroups of 4 waves per CU, ring slots 256-B aligned");
+static_assert(PkLds<8>::TBS == 5 && kWaves * PkLds<8>::WAVE * 4 <= 20480 && PkLds<8>::WAVE % 64 == 0,
+              "8 workgroups of 4 waves per CU, ring slots 256-B aligned");
 
 // SOFT8 traceback of one word (header "Ring and traceback"): A = the lane's emit slot (block k + 1; the
 // convergence block k + 2 is the next slot, +512 B) | 2 for chunk B's half; z[r] = 2 + the position bit of the
@@ -206,6 +201,36 @@ __device__ __forceinline__ uint32_t pk8_traceback(uint32_t base, const uint32_t 
     return __builtin_bitreverse32(nat);  // word bit i <-> stage 63+32k-i
 }
 
+// SOFT4 / FP32 traceback of one word (4-stage fields, nibble g of the ring word; vd_decode_tg's J < 6 recursion:
+// the field's decoded bits are Y = W ^ (T >> 2), the state at the field start ((T << 4) | Y) & 63).  TX = T * 260
+// (T in bits 2..7 and 8..13): the address is ((TX >> sft) & 0xFC) | base as for HARD, and TX >> 4 holds both
+// T >> 2 (bits 0..3) and T's low two bits at bits 4, 5, so Y = ((TX >> 4) ^ W) & 15 and the next state
+// ((TX >> 4) & 0x30) | Y are one v_bitop3_b32 each.  base = the lane's emit slot + 256 for chunk B.
+template <int CORE>
+__device__ __forceinline__ uint32_t pk4_traceback(uint32_t base, const uint32_t (&sft)[3], const uint32_t (&m5)[3])
+{
+    constexpr bool FIX5 = CORE == B32;
+    uint32_t TX = 0, nat = 0;
+    auto step = [&](auto EMc, auto Gc) {
+        constexpr bool EM = decltype(EMc)::value;
+        constexpr int g = decltype(Gc)::value;
+        constexpr int BO = EM ? 0 : 2;
+        constexpr int c = (BO + 4 * g + 3) % 6;
+        constexpr int off = (EM ? 0 : 512) + g / 2;
+        const uint32_t A = __builtin_amdgcn_bitop3_b32(TX >> sft[c / 2], 0xFCu, base, 0xEA);
+        uint32_t W = *(const __attribute__((address_space(3))) uint8_t*)(uintptr_t)(A + off);
+        if constexpr (g % 2) W >>= 4;
+        const uint32_t T4 = TX >> 4;
+        uint32_t Y = __builtin_amdgcn_bitop3_b32(W, T4, 15u, 0x28);  // (W ^ T4) & 15
+        if constexpr (FIX5) Y = __builtin_amdgcn_bitop3_b32(m5[((BO + 4 * g) % 6) / 2], W, Y, 0xCA);
+        if constexpr (!(EM && g == 0)) TX = __mul24(__builtin_amdgcn_bitop3_b32(T4, 0x30u, Y, 0xEA), 260u);
+        if constexpr (EM) nat |= Y << (4 * g);
+    };
+    sfor<8>([&](auto I) { step(std::false_type{}, std::integral_constant<int, 7 - decltype(I)::value>{}); });
+    sfor<8>([&](auto I) { step(std::true_type{}, std::integral_constant<int, 7 - decltype(I)::value>{}); });
+    return __builtin_bitreverse32(nat);  // word bit i <-> stage 63+32k-i
+}
+
 // Split single-batch launches (SPL).  A chunk of W words is cut into P parts at words cut(1) .. cut(P-1),
 // multiples of 3 blocks; part p emits words [cut(p), cut(p+1)).  Part 0 decodes from the chunk start (equal
 // metrics, as the chunk itself); part p >= 1 starts kPkWarm blocks before block cut(p) from equal metrics.
@@ -242,10 +267,9 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(SPL
 {
     constexpr bool P2 = PkFmt<CH>::P2;
     constexpr int J = PkFmt<CH>::J, S = PkFmt<CH>::S;
-    constexpr bool RF = P2 || J == 8;  // ring-first layout (PkLds)
     using IN = TgIn<CH>;
     using TT = TgTabLT<true>;
-    using LL = PkLds<NW, RF>;
+    using LL = PkLds<NW>;
     constexpr bool ALT = CORE == B32;  // M_B32: the upper position half takes the +tag entries at phase 0
     __shared__ __attribute__((aligned(256))) uint32_t lds[kWaves * LL::WAVE];
     const int lane = threadIdx.x & 63;
@@ -255,7 +279,6 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(SPL
     uint32_t* const wlds = lds + wv * LL::WAVE;
     char* const tabb = (char*)(wlds + LL::TAB_OFF);
     uint32_t* const ringA = wlds + LL::RING_OFF;
-    uint32_t* const ringB = ringA + LL::RING;
     // batched: chunks 2w, 2w+1 of the launch (batch b: launch chunks b * nchunks ..; nchunks is even);
     // SPL: chunk w, both halves; tail workgroups: one chunk, wave q its parts 2q, 2q+1
     const bool tail = SPL && blockIdx.x >= geo.tailWG;
@@ -349,12 +372,12 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(SPL
     // traceback roles: lanes 0..31 trace half A's words, 32..63 half B's
     const bool tbB = lane >= 32;
     const uint32_t tbl = (uint32_t)(lane & 31);
-    const char* const tbring = (const char*)(tbB ? ringB : ringA);
     const uint64_t tbStart = tbB ? crB.startWord : crA.startWord;
     const uint32_t tbWords = tbB ? crB.words : crA.words;
-    // RF: the lane's emit-slot LDS address (chunk B: the odd bytes / the high half of each word)
+    // RF: the lane's emit-slot LDS address (chunk B: the odd bytes (HARD) / the high half of each word (SOFT8) /
+    // the slot's second 64 words (SOFT4, FP32))
     const uint32_t tbA2 = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)(const char*)ringA +
-                          512u * tbl + (tbB ? (P2 ? 2u : 1u) : 0u);
+                          512u * tbl + (tbB ? (P2 ? 2u : J == 8 ? 1u : 256u) : 0u);
     // RF: the lane's phase constants for kb = 0 in bytes 0..2 of two words; a pass rotates them by kb % 3 (one
     // v_perm_b32 each with a wave-uniform selector) instead of deriving them from k % 3 per lane.
     //  HARD, q = (k + 1) % 3 (tb_direct): sft = off - 2 = (5, 3, 1) and M_B32's phase-0 masks (0x41, 0x10, 0x04)
@@ -363,6 +386,7 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(SPL
         return __builtin_amdgcn_perm(w, w, r == 0u ? 0x03020100u : r == 1u ? 0x03000201u : 0x03010002u);
     };
     const uint32_t q0 = (tbl + (P2 ? 2u : 1u)) % 3u;
+    // (SOFT4 / FP32: tb_direct<6> offsets, (5, 3, 1) rotated by q, are the shifts themselves: TX = T * 260)
     const uint32_t phA = rot3(P2 ? 0x00060402u : 0x00010305u, q0), phB = P2 ? 0u : rot3(0x00041041u, q0);
 
     typedef uint32_t u2v __attribute__((ext_vector_type(2)));
@@ -447,10 +471,10 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(SPL
 #undef VD_PK_RO8O
                 } else {
                     // bits 1..4 of each half: the even field's as V >> 1, the odd field's (V << 3) into the
-                    // high nibbles of the pair word (chunk A byte 0, chunk B byte 2)
+                    // high nibbles of the pair word (chunk A byte 0, chunk B byte 2) by a v_bitop3_b32 select
                     constexpr uint32_t HN = 0x00F000F0u;
 #define VD_PK_RO4E "v_lshrrev_b32 %[c], 1, %[V]\n\tv_bitop3_b32 %[V], %[V], %[fnm], %[fhf] bitop3:0xea"
-#define VD_PK_RO4O "v_lshlrev_b32 %[t], 3, %[V]\n\tv_bitop3_b32 %[V], %[V], %[fnm], %[fhf] bitop3:0xea\n\tv_bfi_b32 %[c], %[hn], %[t], %[c]"
+#define VD_PK_RO4O "v_lshlrev_b32 %[t], 3, %[V]\n\tv_bitop3_b32 %[V], %[V], %[fnm], %[fhf] bitop3:0xea\n\tv_bitop3_b32 %[c], %[hn], %[t], %[c] bitop3:0xca"
                     uint32_t t;
                     if constexpr (g % 2 == 0)
                         asm(VD_PK_RO4E : [V] "+{v60}"(V), [c] "=&v"(cw[g / 2]) : VD_PK_IN);
@@ -525,13 +549,8 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(SPL
         }
         wave_sync();
         if (j >= 1) {
-            if constexpr (RF) {
-                ringA[(j - 1 - kb) * 128 + ridx] = wA;
-                ringA[(j - 1 - kb) * 128 + 64 + ridx] = wB;
-            } else {
-                ringA[(j - 1 - kb) * 64 + pos] = wA;
-                ringB[(j - 1 - kb) * 64 + pos] = wB;
-            }
+            ringA[(j - 1 - kb) * 128 + ridx] = wA;
+            ringA[(j - 1 - kb) * 128 + 64 + ridx] = wB;
         }
         if (j >= 2 && (j - 1 - kb == tbn || j == nblk - 1)) {
             wave_sync();
@@ -558,8 +577,11 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(SPL
                     const uint32_t m5[3] = {PB, PB >> 8, PB >> 16};
                     w = pk8_traceback<CORE>(tbA2, sft, m5);
                 } else {
-                    const TbC tc = tb_direct<(J < 6 ? 6 : J), CORE == B32>((int)k);
-                    w = traceback_word_tg<J, CORE == B32>(tbring, (tbl + 1u) * 256u, tc);
+                    // (m5 to the field's 4 bits: an even field's byte also holds the odd field's nibble)
+                    const uint32_t PB = rot3(phB, r3);
+                    const uint32_t sft[3] = {PA, PA >> 8, PA >> 16};
+                    const uint32_t m5[3] = {PB & 15u, (PB >> 8) & 15u, (PB >> 16) & 15u};
+                    w = pk4_traceback<CORE>(tbA2, sft, m5);
                 }
                 const uint32_t kc = k + (tbB ? oB : oA);  // chunk word
                 if constexpr (ABL & kAblNoStores) {
@@ -573,13 +595,9 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(SPL
                 }
             }
             wave_sync();
-            if constexpr (RF) {  // block j becomes slot 0 of the next batch
-                ringA[ridx] = wA;
-                ringA[64 + ridx] = wB;
-            } else {
-                ringA[pos] = wA;
-                ringB[pos] = wB;
-            }
+            // block j becomes slot 0 of the next batch
+            ringA[ridx] = wA;
+            ringA[64 + ridx] = wB;
             kb = j - 1;
             tbn = LL::TBS;
         }

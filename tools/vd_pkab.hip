@@ -94,8 +94,7 @@ int main(int argc, char** argv)
     gb.nbatch = (uint32_t)K;
     gb.outStride = ostr;
     const unsigned grid = 800u * (unsigned)K;  // two chunks per wave, 4 waves per workgroup
-    printf("TBS: 8 waves %d, 7 waves %d, 6 waves %d (SOFT8 layout %d %d %d)\n", vd::PkLds<8>::TBS, vd::PkLds<7>::TBS, vd::PkLds<6>::TBS,
-           vd::PkLds<8, true>::TBS, vd::PkLds<7, true>::TBS, vd::PkLds<6, true>::TBS);
+    printf("TBS: 8 waves %d, 7 waves %d, 6 waves %d\n", vd::PkLds<8>::TBS, vd::PkLds<7>::TBS, vd::PkLds<6>::TBS);
     const Variant vs[] = {VD_PKAB_VARIANTS};
     const int nv = sizeof(vs) / sizeof(vs[0]);
     hipEvent_t ev[4];
