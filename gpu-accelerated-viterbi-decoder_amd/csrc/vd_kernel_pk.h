@@ -4,60 +4,58 @@
 // (reference viterbi_core, src/viterbi/viterbi.cu:144-207; tie rules viterbiACS.cuh:113-157,216-256; the
 // int16x2 idea of selfPM/pairPM<M_B16>, viterbiACS.cuh:113-119,216-220).
 //
-// Why it is exact.  A HARD metric needs few bits: every path metric lies within D = 12 units of the best
-// one and the best grows by at most 1 unit per stage, so R stages after a renormalisation the candidates of
-// a stage stay within [-14, D + R + 2] units of position 0's metric (vd_kernel_tg.h "Range").  With the
-// tagged scheme of the int32 patterns (TgFmt::INT: V = BASE + metric * 2^9 + 2^8 + h, 8-stage history
-// fields, |h| < 2^8) and one renormalisation per 96-stage group (R = 96: [-14, 110] units) every value a
-// stage computes lies in BASE + [-14 * 512, 111 * 512): with BASE = 7680, in [512, 64512), inside an
-// unsigned 16-bit half.  Two chunks' metrics VA, VB sit in one 32-bit word
-// V = VB * 2^16 + VA, and a table entry holds both chunks' entries as m = EB * 2^16 + EA (signed halves).
-// 32-bit integer addition is a ring homomorphism: V + m = (VB + EB) * 2^16 + (VA + EA) exactly, and the
-// word's halves ARE VA + EA and VB + EB whenever both lie in [0, 2^16) -- which the bound guarantees for
-// every sum the kernel forms (the intermediate carries of two's-complement halves cancel modulo 2^32).
-// SOFT4 / FP32 (BMmax 16, D = 192: candidates within [-209, +723] units) fit with 4-stage fields, S = 5:
-// BASE = 8192, values in [1504, 31328).
-//
-// SOFT8 range (round 5).  BM = +-s0 +- s1 with s in [-128, 127]: BMmax 256, and two labels differing in one
-// output bit differ by 2|s| <= 256.  The spread of the metrics is at most 256 w, w = 11: PM[T1] - PM[T2] is at
-// most the BM difference along the two 6-stage paths into T1 and T2 from T1's survivor origin, i.e. 256 times
-// the Hamming weight of the first six output pairs of the code driven by T1 ^ T2 from the zero state, at most
-// 11 for (0171, 0133) (a chunk's first stages from equal metrics: at most 2 per stage, 10) -- D = 2816 instead
-// of (K-1)(BMmax - BMmin) = 3072.  Renormalising every R = 8 stages, the candidates of a stage lie within
-// [-D - 256, D + 8 * 256] = [-3072, 4864] units of position 0's metric: 7,937 units, so 2-stage history
-// fields (S = 3, tags -+1, -+2) fit a 16-bit half: BASE = 25600, values in [1024, 64520).
+// Why it is exact.  R stages after a renormalisation (position 0's metric subtracted from every lane) every
+// metric lies within [-D, D + (R-1) BMmax] of position 0's: the largest never decreases, grows by at most
+// BMmax per stage, and every metric is within D of it.  A candidate's metric part is a metric plus a branch
+// metric, so within [-(D + BMmax), D + R BMmax] units of 2^S, and the history field (tags included) adds
+// [0, 2^S).  With V = BASE + metric * 2^S + field (vd_decode_tg's INT tagged scheme, J-stage fields, S = J + 1)
+// that range sits inside an unsigned 16-bit half (tests/test_metric_range.py::test_packed_halves_fit):
+//   HARD   BMmax 1, D 12, J 8, S 9, R 96 (once per group), BASE 7680: values in [1024, 63488);
+//   SOFT4 / FP32   BMmax 16, D 192, J 4, S 5, R 32, BASE 8192: values in [1536, 30752);
+//   SOFT8  BMmax 256, D 2816, J 2, S 3, R 8, BASE 25600: values in [1024, 64520).
+// SOFT8's D: two labels differing in one output bit differ by 2|s| <= 256, and PM[T1] - PM[T2] is at most the
+// BM difference along the two 6-stage paths into T1 and T2 from T1's survivor origin, i.e. 256 times the
+// Hamming weight of the first six output pairs of the code driven by T1 ^ T2 from the zero state, at most 11
+// for (0171, 0133): D = 2816 instead of (K-1)(BMmax - BMmin) = 3072, which would not fit 2-stage fields.
+// Two chunks' metrics VA, VB sit in one 32-bit word V = VB * 2^16 + VA, and a table entry holds both chunks'
+// entries as the integer m = EB * 2^16 + EA (signed halves).  32-bit integer addition is a ring homomorphism:
+// V + m = (VB + EB) * 2^16 + (VA + EA) exactly, and the word's halves ARE VA + EA and VB + EB whenever both
+// lie in [0, 2^16) -- which the bound guarantees for every sum the kernel forms.
 //
 // So one v_add_u32 / v_sub_u32 adds for both chunks, v_pk_max_u16 takes both maxima, and the DPP exchange
 // rides on the subtraction (v_sub_u32_dpp: the partner's V minus the shared entry).  A DPP stage is
 // v_add_u32 + v_sub_u32_dpp + v_pk_max_u16 for two chunk-states, an LDS-exchange stage v_sub_u32 +
-// v_add_u32 + v_pk_max_u16 with one crossbar round trip for both chunks; renormalisation is the int32
-// kernels' readfirstlane / s_sub / v_subrev on the whole word (again a homomorphism).
+// v_add_u32 + v_pk_max_u16 with one crossbar round trip for both chunks; renormalisation is readfirstlane /
+// s_sub / v_subrev (or v_xad) on the whole word (again a homomorphism).
 //
 // Batched: the two chunks of a wave are consecutive chunks 2w, 2w+1 of the launch (the same batch: 6400 is
-// even); they decode in lockstep over the longer one's blocks, each emitting only its own words.  LDS per wave:
-// [guard | label-region table with the +tag area (TgTabLT<true>) | guard | ring A | ring B | guard]; two
-// rings in a wave's 5,120 B leave 6 slots each, so a traceback batch traces 5 words per chunk, both chunks'
+// even); they decode in lockstep over the longer one's blocks, each emitting only its own words.  LDS per wave
+// (PkLds): [ring | guard | label-region table with the +tag area (TgTabLT<true>) | guard | guard]; 6 ring slots
+// of 512 B (both chunks) in a wave's 5,120 B, so a traceback batch traces 5 words per chunk, both chunks'
 // words in one pass (lanes 0..4 chunk A, lanes 32..36 chunk B).
 //
 // Read-out.  Every field clear is (V & ~field) | base as one v_bitop3_b32 (2 cycles; v_and_or_b32 takes 4,
-// profiles/r05/ubench12.log).  J = 8 (HARD): SDWA shifts each half's field bits into byte g of its chunk's ring word.  J = 4
-// (SOFT4 / FP32): nibble g of the ring word; field pairs are gathered as c = (V >> 1) of the even field,
-// bfi(0x00F000F0, V << 3, c) of the odd one (chunk A's two fields in byte 0, chunk B's in byte 2), and at
-// the block end four v_perm_b32 turn the four pair words into the two ring words.
-// J = 2 (SOFT8): after a field F = 4 + h is odd, its take-bits d = bits 1, 2.  x = V & 0x00060006 (both
-// halves, v_and_b32), V = (V & ~7) | 4 per half (v_bitop3_b32) puts F back to 4; every fourth field instead
-// V = (V ^ x) + VBASE - 0x00010001 - (V of position 0 & ~7 in each half) (v_xad_u32, the constant on the
-// scalar unit) clears and renormalises at once; v_lshl_or_b32 collects d into bits 2g of two pair words
-// (fields 0..7 and 8..15; chunk A low, chunk B high half) that are the block's two ring words as they stand --
-// 3 VALU per field for both chunks, 8 cycles (v_and_b32 and v_bitop3_b32 issue in 2, profiles/r05/ubench12.log).
-// Ring and traceback (SOFT8).  The ring is indexed by p' = rotl6(p, 1), where the two stages of a field
-// (t0 even, t0 + 1) flip position bits q' = t0 % 6 and t0 % 6 + 1 (never wrapping).  Tracing back is then
-// position arithmetic: from p' = 0 (state 0) at a block end, each field back is p' ^= d << (t0 % 6), and the
-// field's two decoded bits are bits t0 % 6, t0 % 6 + 1 of the new p' (the stored bit of an M_B32 phase-0 stage
-// in the upper position half, an own-won tag, is complemented once per block so that every stored bit is a
-// take-bit).  A lane keeps its LDS read address A = slot | 4 p' (ring slots 256-B aligned: the ring leads the
-// wave's LDS), so a step is one ds_read_u8_d16_hi at a constant offset and three 2-cycle VALU ops (pk2_traceback):
-// 32 dependent steps per word (tools/pk2_model.py replays the scheme against the reference).
+// profiles/r05/ubench12.log).
+//  * J = 8 (HARD): x = V >> 1 puts each half's take-bits in bytes 0 and 2; an odd field's x and the even
+//    field's before it become ring word g / 2 = [B odd, A odd, B even, A even] by one v_perm_b32.
+//  * J = 4 (SOFT4 / FP32): nibble g of the ring word; field pairs are gathered as c = (V >> 1) of the even
+//    field and (V << 3) of the odd one selected into the high nibbles (v_bitop3_b32; chunk A's two fields in
+//    byte 0, chunk B's in byte 2), and at the block end four v_perm_b32 turn the four pair words into the two
+//    ring words.
+//  * J = 2 (SOFT8): after a field F = 4 + h is odd, its take-bits d = bits 1, 2.  x = V & 0x00060006 (both
+//    halves, v_and_b32), V = (V & ~7) | 4 per half (v_bitop3_b32) puts F back to 4; every fourth field instead
+//    V = (V ^ x) + VBASE - 0x00010001 - (V of position 0 & ~7 in each half) (v_xad_u32, the constant on the
+//    scalar unit) clears and renormalises at once; v_lshl_or_b32 collects d into bits 2g of two pair words
+//    (fields 0..7 and 8..15; chunk A low, chunk B high half) that are the block's two ring words as they stand.
+// Tracebacks (2-cycle VALU ops but a multiply and a perm per field; the per-pass phase constants rotated by
+// one v_perm_b32): pk8_traceback (HARD), pk4_traceback (SOFT4 / FP32), pk2_traceback (SOFT8: position space.
+// The ring is indexed by p' = rotl6(p, 1), where the two stages of a field (t0 even, t0 + 1) flip position bits
+// q' = t0 % 6 and t0 % 6 + 1 (never wrapping).  Tracing back is then position arithmetic: from p' = 0 (state
+// 0) at a block end, each field back is p' ^= d << (t0 % 6), and the field's two decoded bits are bits
+// t0 % 6, t0 % 6 + 1 of the new p' (the stored bit of an M_B32 phase-0 stage in the upper position half, an
+// own-won tag, is complemented once per block so that every stored bit is a take-bit).  A lane keeps its LDS
+// read address A = slot | 4 p', so a step is one ds_read_u8_d16_hi at a constant offset and three 2-cycle
+// VALU ops: 32 dependent steps per word; tools/pk2_model.py replays the scheme against the reference).
 #pragma once
 #include "vd_kernel_tg.h"
 
