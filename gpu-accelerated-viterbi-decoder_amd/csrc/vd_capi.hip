@@ -142,9 +142,8 @@ launch_fn pick_pk_ch(int o)
     switch (ch_of(o)) {
     case 0: return pick_pk_ob<L + vd::HARD, SPL>(o);
     case 1: return pick_pk_ob<L + vd::SOFT4, SPL>(o);
-    // SOFT8 batched only: its split single-batch launch re-decodes nearly every chunk on noise-like input
-    // (the speculative second part rarely converges on saturated random values: 0.36 against 0.19 ms), and on
-    // codewords it measured no faster than vd_decode_tg's segment launch (0.182 against 0.181 ms)
+    // (SOFT8 single batches: the split kernel is 9 % faster than vd_decode_tg's segment launch on codewords
+    // and, with the early-stop re-decodes, 18 % slower on noise-only input: DESIGN.md 4.3)
     case 2:
         return out_of(o) == 1 ? (met_of(o) == 0 ? &launch_pk<L + vd::SOFT8, 0, 16, SPL> : &launch_pk<L + vd::SOFT8, 1, 16, SPL>)
                               : (met_of(o) == 0 ? &launch_pk<L + vd::SOFT8, 0, 32, SPL> : &launch_pk<L + vd::SOFT8, 1, 32, SPL>);
@@ -193,10 +192,10 @@ const char* kname(int o)
          "vd_decode_tg<SOFT4,B16> (single batches with chunks under 64 words); M_B16 tie rule",
          "vd_decode_pk<SOFT4,F16> (int16 halves: batched, two chunks per lane; single batch, one chunk cut in two) / "
          "vd_decode_tg<SOFT4,F16> (single batches with chunks under 64 words); M_FP16 tie rule"},
-        {"vd_decode_pk<SOFT8,B32> (int16 halves, 2-stage fields: batched, two chunks per lane) / "
-         "vd_decode_tg<SOFT8,B32> (fp32 tagged core: single batches, segment launch); M_B32 tie rule",
-         "vd_decode_pk<SOFT8,B16> (int16 halves, 2-stage fields: batched, two chunks per lane) / "
-         "vd_decode_tg<SOFT8,B16> (fp32 tagged core: single batches, segment launch); M_B16 tie rule",
+        {"vd_decode_pk<SOFT8,B32> (int16 halves, 2-stage fields: batched, two chunks per lane; single batch, one "
+         "chunk cut in two) / vd_decode_tg<SOFT8,B32> (single batches with chunks under 64 words); M_B32 tie rule",
+         "vd_decode_pk<SOFT8,B16> (int16 halves, 2-stage fields: batched, two chunks per lane; single batch, one "
+         "chunk cut in two) / vd_decode_tg<SOFT8,B16> (single batches with chunks under 64 words); M_B16 tie rule",
          "-"},
         {"vd_decode_tg<SOFT16,B32> (int32 tagged patterns, M_B32 tie rule)", "-", "-"},
         {"vd_decode_pk<FP32,B32> (int16 halves: batched, two chunks per lane; single batch, one chunk cut in two) / "
@@ -243,7 +242,7 @@ struct vd_decoder {
     DeviceState* ds = nullptr;  // the device's board / segment tables (looked up once, vd_create)
     int split = 1;              // segment launches: 0 none (VD_NO_SPLIT=1), 1 pieces, 2 thirds, 3 sevenths (VD_SPLIT=...)
     int pk = 1;                 // HARD/SOFT4/FP32 launches on vd_decode_pk (VD_NO_PK=1: on vd_decode_tg)
-    int pksplit = 1;            // their single-batch launches split on vd_decode_pk (VD_PK_SPLIT=0: tg segments; 2: SOFT8 too)
+    int pksplit = 1;            // their single-batch launches split on vd_decode_pk (VD_PK_SPLIT=0: tg segments)
     int pktail = 1;             // ... with the tail chunks in 4-wave workgroups (VD_PK_TAIL=0: one chunk per wave)
     uint32_t* check = nullptr;  // LDS guard violation counter (vd_set_guard_check), null = off
 };
@@ -331,7 +330,7 @@ static unsigned plan_split(vd::Geom& g, int options, const DeviceState* x, int m
 
 // Which kernel and launch form a decode takes (launch_decode and vd_decoder_kernel_name share it):
 // batched launches of HARD/SOFT4/SOFT8/FP32 on vd_decode_pk (two chunks per wave); single batches of
-// HARD/SOFT4/FP32 with chunks of >= kSplitMinWords words on vd_decode_pk's split kernel; the rest on
+// HARD/SOFT4/SOFT8/FP32 with chunks of >= kSplitMinWords words on vd_decode_pk's split kernel; the rest on
 // vd_decode_tg (segment launch when plan_split finds a table, else one chunk per wave).
 enum class Form { PkBatched, PkSplit, Tg };
 static Form plan_form(const vd_decoder* d, uint64_t packNum, uint32_t nbatch, bool llr)
@@ -341,7 +340,7 @@ static Form plan_form(const vd_decoder* d, uint64_t packNum, uint32_t nbatch, bo
     const uint64_t w32 = out_of(options) != 0 ? packNum / 2 : packNum;
     const bool splitok = nbatch == 1 && d->pk && d->pksplit && d->split && vd::kChunks % vd::kWaves == 0 &&
                          w32 / vd::kChunks >= (uint64_t)vd::kSplitMinWords;
-    if (splitok && (ch_of(options) != 2 || d->pksplit == 2) && pick_pk<true>(options, llr)) return Form::PkSplit;
+    if (splitok && pick_pk<true>(options, llr)) return Form::PkSplit;
     return Form::Tg;
 }
 
@@ -476,7 +475,7 @@ int vd_create(int options, size_t preallocInputNum, int device, vd_decoder** out
     const char* nopk = std::getenv("VD_NO_PK");
     d->pk = nopk && nopk[0] == '1' ? 0 : 1;
     const char* pks = std::getenv("VD_PK_SPLIT");
-    d->pksplit = pks && pks[0] == '0' ? 0 : pks && pks[0] == '2' ? 2 : 1;
+    d->pksplit = pks && pks[0] == '0' ? 0 : 1;
     const char* pkt = std::getenv("VD_PK_TAIL");
     d->pktail = pkt && pkt[0] == '0' ? 0 : 1;
     const char* chk = std::getenv("VD_CHECK");

@@ -127,11 +127,10 @@ def test_packed_split_random_input_redecodes(gpu, vo, opt):
     """Uniformly random channel words: the second part's speculative start often does not converge (HARD:
     652 of 6400 chunks on the first run; SOFT8 about a fifth of the parts), so re-decodes run -- most of them
     stopping at a checkpoint one or two groups after the cut (vd_kernel_pk.h "Early stop"), the rest decoding
-    the whole part -- and the words still equal the oracle's.  SOFT8 splits on the packed kernel only with
-    VD_PK_SPLIT=2."""
+    the whole part -- and the words still equal the oracle's."""
     nbits = 16_000_000
     n = 2 * nbits
-    env = {"VD_PK_SPLIT": "2"} if (opt & 7) == SOFT8 else {}
+    env = {}
     nin = gpu.lib().vd_input_size(opt, n)
     g = torch.Generator(device="cpu").manual_seed(5)
     packed = torch.randint(0, 256, (nin + 256,), dtype=torch.uint8, generator=g).to("cuda")
@@ -152,13 +151,13 @@ def test_packed_split_random_input_redecodes(gpu, vo, opt):
 @pytest.mark.parametrize("opt", [SOFT8 | M_B16, SOFT8 | M_B32, SOFT8 | M_B16 | O_B16], ids=name)
 @pytest.mark.parametrize("nbits,snr", [(13_107_264, 1.0), (20_000_000, 0.0), (32_000_000, 15.0)])
 def test_packed_split_soft8(gpu, vo, opt, nbits, snr):
-    """SOFT8 single-batch launches split on vd_decode_pk (VD_PK_SPLIT=2): equal to the oracle, to the default
-    segment launch on vd_decode_tg and to the split launch without tail workgroups."""
+    """SOFT8 single-batch launches split on vd_decode_pk: equal to the oracle, to vd_decode_tg's segment launch
+    (VD_PK_SPLIT=0) and to the split launch without tail workgroups."""
     n = 2 * nbits
     packed, stride, nin = _batches(gpu, opt, nbits, snr, 1, 93)
-    pk = _single(gpu, opt, packed, nin, n, {"VD_PK_SPLIT": "2"})
-    tg = _single(gpu, opt, packed, nin, n, {})
-    notail = _single(gpu, opt, packed, nin, n, {"VD_PK_SPLIT": "2", "VD_PK_TAIL": "0"})
+    pk = _single(gpu, opt, packed, nin, n, {})
+    tg = _single(gpu, opt, packed, nin, n, {"VD_PK_SPLIT": "0"})
+    notail = _single(gpu, opt, packed, nin, n, {"VD_PK_TAIL": "0"})
     p = packed[:nin].cpu().numpy().view(np.int32)
     ref, ok = vo.decode(opt, p, input_num=n, nthreads=16)
     got = pk.cpu().numpy().view(ref.dtype)

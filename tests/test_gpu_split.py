@@ -4,7 +4,7 @@ chunks in 4 segments that cross chunk boundaries).  A segment that starts inside
 speculatively and is checked at its boundary after a workgroup barrier; one whose check fails
 re-decodes from its left neighbour's end vector.  The decoded words must be identical to the unsplit launch (VD_NO_SPLIT=1) and
 to the oracle, at SNRs where the speculation always converges and where it often does not (SNR 0: the
-re-decode passes run, and the test requires that they did).  HARD, SOFT4 and FP32 single launches run
+re-decode passes run, and the test requires that they did).  HARD, SOFT4, SOFT8 and FP32 single launches run
 vd_decode_pk's split launch by default (mode "pk": one chunk per wave, its second part in the other int16
 half with a speculative start, checked at the cut, re-decoded from the first part's vector when it
 differs); "pieces" / "thirds" set VD_PK_SPLIT=0 to test vd_decode_tg's segment tables on them too."""
@@ -17,11 +17,11 @@ from vitdec import FP32, HARD, M_B16, M_B32, M_FP16, O_B16, SOFT4, SOFT8, SOFT16
 from test_gpu_parity import gpu_decode, name
 
 
-PK_CH = (HARD, SOFT4, FP32)
+PK_CH = (HARD, SOFT4, SOFT8, FP32)
 
 
 def set_mode(mode):
-    """environment of a decoder created next: 'pk' = the default (vd_decode_pk split for HARD/SOFT4/FP32),
+    """environment of a decoder created next: 'pk' = the default (vd_decode_pk split for HARD/SOFT4/SOFT8/FP32),
     'pieces' / 'thirds' = vd_decode_tg segment tables for every format"""
     if mode in ("pieces", "thirds"):
         os.environ["VD_SPLIT"] = mode
