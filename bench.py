@@ -465,15 +465,16 @@ def single_launch_side_measurement(batches, stream, sptr, reps=20, keep=None):
 
 
 def llr_side_measurement(dev, sptr, stream, reps=20, keep=None):
-    """Float channel values in HBM (the reference's AddNoise output, before SoftDecisionPacker): the GPU
-    packer alone, packer + decode, and the fused decode (quantisation in the table build), SOFT8/int16.
-    Outside the timed region; not part of `value`."""
+    """Float channel values in HBM (the reference's AddNoise output before SoftDecisionPacker: the harness
+    chain's codeword + AWGN at SNR_DB, vd_channel_device): the GPU packer alone, packer + decode, and the fused
+    decode (quantisation in the table build), SOFT8/int16.  Outside the timed region; not part of `value`.
+    (Until round 5 the values were random +-1 symbols plus noise, not a codeword: noise to the decoder, on
+    which speculative split starts rarely converge.)"""
     opt = vitdec.SOFT8 | vitdec.M_B16 | vitdec.O_B32
     n = 2 * N_BITS
-    g = torch.Generator(device=dev)
-    g.manual_seed(5)
-    vals = (torch.randint(0, 2, (n,), device=dev, generator=g).float() * 2 - 1
-            + 0.5 * torch.randn(n, device=dev, generator=g))
+    vals = torch.empty(n, dtype=torch.float32, device=dev)
+    src = torch.empty(N_BITS, dtype=torch.uint8, device=dev)
+    vitdec.channel_device(N_BITS, SNR_DB, 901, 902, src.data_ptr(), vals.data_ptr(), sptr)
     packed = torch.empty(vitdec.lib().vd_input_size(opt, n), dtype=torch.uint8, device=dev)
     out_fused = torch.empty(vitdec.lib().vd_output_size(opt, n), dtype=torch.uint8, device=dev)
     out_two = torch.empty_like(out_fused)
@@ -501,8 +502,8 @@ def llr_side_measurement(dev, sptr, stream, reps=20, keep=None):
     many = torch.empty(reps * n, dtype=torch.float32, device=dev)
     many[:n] = vals
     for k in range(1, reps):
-        many[k * n:(k + 1) * n] = (torch.randint(0, 2, (n,), device=dev, generator=g).float() * 2 - 1
-                                   + 0.5 * torch.randn(n, device=dev, generator=g))
+        vitdec.channel_device(N_BITS, SNR_DB, 901 + 2 * k, 902 + 2 * k, src.data_ptr(), many[k * n:].data_ptr(), sptr)
+    del src
     nout = out_fused.numel()
     ostride = (nout + 255) // 256 * 256
     outs = torch.empty(reps * ostride, dtype=torch.uint8, device=dev)
@@ -522,7 +523,8 @@ def llr_side_measurement(dev, sptr, stream, reps=20, keep=None):
                      outs[(reps - 1) * ostride:(reps - 1) * ostride + nout].cpu().numpy(), n, 40000.0))
     dec.close()
     del many, outs
-    return {"workload": "64M float32 channel values (32M-bit SOFT8 batch, scale 40000) resident in HBM",
+    return {"workload": "64M float32 channel values (the harness's codeword + AWGN at %.1f dB, 32M-bit SOFT8 batch, "
+                        "scale 40000) resident in HBM" % SNR_DB,
             "pack_ms": round(t_pack, 4), "pack_GBps": round(n * 4 / (t_pack * 1e-3) / 1e9, 1),
             "pack_then_decode_ms": round(t_two, 4), "fused_decode_ms": round(t_fused, 4),
             "fused_gbps": round(msg / (t_fused * 1e-3) / 1e9, 2), "fused_equals_pack_then_decode": same,
