@@ -244,13 +244,20 @@ __device__ __forceinline__ uint32_t pk4_traceback(uint32_t base, const uint32_t 
 //  * The last nchunks mod 4 NCU chunks (tail workgroups, Geom::tailWG): one chunk per workgroup of 4 waves,
 //    P = 8, so every SIMD gets 6 whole-chunk waves and one short one instead of 7 whole-chunk waves on a
 //    quarter of the SIMDs; the end vectors cross waves through LDS after a workgroup barrier.
-// Early stop.  Every run of a part p >= 1 also keeps its vectors at the kPkChk group ends after its cut
-// (chunk blocks cut(p) - 1 + 3m, m = 1 .. kPkChk: checkpoint m).  A re-decode compares its vector there with
-// the kept one, which belongs to the run whose words currently stand after that block: equal vectors mean
-// equal decisions from the next block on, so the re-decode only has to emit the words whose traceback
-// windows reach back to the checkpoint block s or earlier (local words < s) and stops after block s + 1.
+// Early stop.  A re-decode only has to run until its metric vector equals, at some group end s after the cut,
+// the vector of the run whose words currently stand after s: equal vectors mean equal decisions from block
+// s + 1 on, so it emits the words whose traceback windows reach back to block s or earlier (local words < s)
+// and stops after block s + 1.  The vectors to compare with come from one of two places:
+//  * replay (one half re-decodes for the first time, the other is idle: every re-decode of a whole-chunk
+//    wave): both halves
+//    restart 6 blocks before the cut from equal metrics, the idle half replaying the speculative run
+//    exactly (same inputs, same arithmetic per half), the re-decoding half with the correct vector put in
+//    at the cut; the two halves are compared at every group end after the cut;
+//  * checkpoints (otherwise: tail workgroups only): every run of a part p >= 1 keeps its vectors
+//    at the kPkChk group ends after its cut (chunk blocks cut(p) - 1 + 3m, m = 1 .. kPkChk) in registers.
 // On uniformly random input 78 % of 6-block warm-ups converge, 96.5 % after one more group, 99.5 % after
-// two (tools/study/spec_convergence.py): most re-decodes then take 3 or 6 blocks instead of a whole part.
+// two, all 400 samples within 7 (tools/study/spec_convergence.py); at 0 dB 95 % at the cut, the rest one
+// group later.
 constexpr int kPkWarm = 6;
 constexpr int kPkChk = 2;
 __host__ __device__ constexpr uint32_t pk_cut(uint32_t p, uint32_t P, uint32_t W)
@@ -326,9 +333,12 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(SPL
     const uint32_t P = tail ? 2u * kWaves : 2u, pA = tail ? 2u * (uint32_t)wv : 0u, pB = pA + 1u;
     uint32_t oA = 0, oB = 0, kminA = 0, kmaxA = WA, kminB = 0, kmaxB = WB;
     uint32_t ssA = ~0u, seA = ~0u, ssB = ~0u, seB = ~0u;
-    // SPL early stop: local block of checkpoint 1 per half (~0u: none) and whether this run compares there
+    // SPL early stop: local block of checkpoint 1 per half (~0u: none) and whether this run compares there;
+    // replay mode: 1 = half A re-decodes (B replays), 2 = half B re-decodes (A replays); its vector at the cut
+    // is its kept start vector (A: sv2 low, B: sv1 high)
     uint32_t ckA = ~0u, ckB = ~0u;
     bool rdA = false, rdB = false;
+    uint32_t rpl = 0;
     if constexpr (SPL) {
         const uint32_t cA0 = pk_cut(pA, P, WA), cA1 = pk_cut(pA + 1u, P, WA), cB1 = pk_cut(pB + 1u, P, WA);
         oA = pA ? cA0 - kPkWarm : 0u;
@@ -523,6 +533,15 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(SPL
             if (j == seB) sv2 = __builtin_amdgcn_perm(V, sv2, 0x07060100u);
             if constexpr (PH == 4) {  // checkpoints are group ends (header "Early stop")
                 bool stop = false;
+                if (rpl) {
+                    if (j == kPkWarm - 1u) {  // the cut: the re-decoding half takes the correct vector
+                        V = rpl == 1u ? __builtin_amdgcn_perm(V, sv2, 0x07060100u) : __builtin_amdgcn_perm(sv1, V, 0x07060100u);
+                    } else if (j > kPkWarm - 1u && __builtin_amdgcn_ballot_w64((V & 0xFFFFu) != (V >> 16)) == 0) {
+                        if (rpl == 1u) kmaxA = kmaxA < j ? kmaxA : j;
+                        else kmaxB = kmaxB < j ? kmaxB : j;
+                        stop = true;
+                    }
+                }
                 sfor<kPkChk>([&](auto Mc) {
                     constexpr int m = decltype(Mc)::value;
                     if (j == ckA + 3u * m) {
@@ -715,6 +734,33 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(SPL
         // decode again every part whose start vector differs, from block cut(p) with the left end vector;
         // an idle half repeats the other half's job without writing or keeping vectors
         uint32_t vA = 0, vB = 0;
+        // (replay only for a part's first re-decode: the run it replays must be the one whose words stand)
+        rpl = pass == 0u && mA != mB ? (mA ? 1u : 2u) : 0u;
+        if (rpl) {  // replay (header "Early stop"): both halves from 6 blocks before the re-decoding part's cut
+            const uint32_t p = mA ? pA : pB;
+            const uint32_t o = pk_cut(p, P, WA) - kPkWarm, km = pk_cut(p + 1u, P, WA) - o;
+            const uint32_t vin = mA ? nb >> 16 : sv1 & 0xFFFFu;
+            oA = oB = o;
+            kminA = kmaxA = kminB = kmaxB = 0;
+            ssA = seA = ssB = seB = ~0u;
+            ckA = ckB = ~0u;  // the re-decoding half keeps its checkpoint vectors (no comparison there)
+            rdA = rdB = false;
+            if (mA) {
+                kminA = kPkWarm;
+                kmaxA = km;
+                seA = km - 1u;
+                ckA = kPkWarm + 2u;
+                sv2 = __builtin_amdgcn_perm(sv2, vin, 0x07060100u);  // its start vector
+            } else {
+                kminB = kPkWarm;
+                kmaxB = km;
+                seB = pB + 1u < P ? km - 1u : ~0u;
+                ckB = kPkWarm + 2u;
+                sv1 = __builtin_amdgcn_perm(vin << 16, sv1, 0x07060100u);
+            }
+            V = VBASE;
+            nblk = km + 2u;
+        } else {
         rdA = mA;
         rdB = mB;
         ckA = mA ? 2u : ~0u;
@@ -752,6 +798,7 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(SPL
         V = vA | vB << 16;
         nblk = mA || mB ? (mA ? kmaxA : kmaxB) + 2u : 0u;
         if (mA && mB && kmaxB > kmaxA) nblk = kmaxB + 2u;
+        }
         startA = stA + 32ull * oA;
         startB = stB + 32ull * oB;
         kb = 0;

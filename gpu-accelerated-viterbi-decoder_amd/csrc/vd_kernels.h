@@ -139,6 +139,7 @@ __device__ __forceinline__ uint32_t simd_slot()
 struct Fair {
     uint32_t* mine = nullptr;   // this wave's word
     uint32_t* simd = nullptr;   // the SIMD's kFairWaves words
+    __amdgpu_buffer_rsrc_t rs;  // ... as a buffer resource (SGPRs: the per-lane read needs one offset VGPR)
     uint32_t seen = kFairEmpty; // lane l < kFairWaves: word l as read at the previous group head
     uint32_t last = kFairEmpty; // this wave's value posted at the previous call
 
@@ -148,6 +149,7 @@ struct Fair {
         const uint32_t wid = __builtin_amdgcn_s_getreg(4 | (0 << 6) | (31 << 11)) & (kFairWaves - 1);
         simd = board + (size_t)simd_slot() * kFairWaves;
         mine = simd + wid;
+        rs = __builtin_amdgcn_make_buffer_rsrc(simd, (short)0, (int)(kFairWaves * 4), 0x00020000);
         if (lane == 0) __hip_atomic_store(mine, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
     }
     // group head: now = progress so far, unit3 = the progress of 3 blocks (the priority step); both in the
@@ -175,8 +177,8 @@ struct Fair {
         }
         if (lane == 0) __hip_atomic_store(mine, now, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
         last = now;
-        const uint32_t* w = simd + (lane & (kFairWaves - 1));
-        seen = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        // (glc: past the CU's L1, as the relaxed atomic load it replaces)
+        seen = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rs, (uint32_t)(lane & (kFairWaves - 1)) * 4u, 0, 1);
     }
     __device__ __forceinline__ void end(int lane)
     {
