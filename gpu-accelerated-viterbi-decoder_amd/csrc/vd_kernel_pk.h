@@ -360,7 +360,7 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(SPL
     // SPL: kept vectors, one per half: sv1 = (A's end, B's start), sv2 = (A's start, B's end) (low, high);
     // cpv[m]: the halves' vectors at checkpoint m + 1
     uint32_t sv1 = 0, sv2 = 0;
-    uint32_t cpv[kPkChk] = {};
+    uint32_t cpv[kPkChk > 0 ? kPkChk : 1] = {};
     uint32_t kb = 0;
     uint32_t sink = 0;  // kAblNoStores
     uint32_t tbn = LL::TBS - (blockIdx.x & 3u) % LL::TBS;  // staggered first traceback batches
