@@ -527,15 +527,20 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(SPL
             wB = ~wB;
         }
         if constexpr (SPL) {  // kept vectors (block ends: renormalised, fields cleared)
-            if (j == seA) sv1 = __builtin_amdgcn_perm(sv1, V, 0x07060100u);  // low half from V
-            if (j == ssB) sv1 = __builtin_amdgcn_perm(V, sv1, 0x07060100u);  // high half from V
-            if (j == ssA) sv2 = __builtin_amdgcn_perm(sv2, V, 0x07060100u);
-            if (j == seB) sv2 = __builtin_amdgcn_perm(V, sv2, 0x07060100u);
+            // (VD_RARE: a real branch -- left alone the compiler turns these rare wave-uniform updates into
+            // v_cndmask selects executed at every block end, about 18 cycles each at 8 waves per SIMD)
+#define VD_RARE asm volatile("")
+            if (j == seA) { VD_RARE; sv1 = __builtin_amdgcn_perm(sv1, V, 0x07060100u); }  // low half from V
+            if (j == ssB) { VD_RARE; sv1 = __builtin_amdgcn_perm(V, sv1, 0x07060100u); }  // high half from V
+            if (j == ssA) { VD_RARE; sv2 = __builtin_amdgcn_perm(sv2, V, 0x07060100u); }
+            if (j == seB) { VD_RARE; sv2 = __builtin_amdgcn_perm(V, sv2, 0x07060100u); }
             if constexpr (PH == 4) {  // checkpoints are group ends (header "Early stop")
                 bool stop = false;
                 if (rpl) {
                     if (j == kPkWarm - 1u) {  // the cut: the re-decoding half takes the correct vector
-                        V = rpl == 1u ? __builtin_amdgcn_perm(V, sv2, 0x07060100u) : __builtin_amdgcn_perm(sv1, V, 0x07060100u);
+                        VD_RARE;
+                        if (rpl == 1u) V = __builtin_amdgcn_perm(V, sv2, 0x07060100u);
+                        else V = __builtin_amdgcn_perm(sv1, V, 0x07060100u);
                     } else if (j > kPkWarm - 1u && __builtin_amdgcn_ballot_w64((V & 0xFFFFu) != (V >> 16)) == 0) {
                         if (rpl == 1u) kmaxA = kmaxA < j ? kmaxA : j;
                         else kmaxB = kmaxB < j ? kmaxB : j;
@@ -545,6 +550,7 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(SPL
                 sfor<kPkChk>([&](auto Mc) {
                     constexpr int m = decltype(Mc)::value;
                     if (j == ckA + 3u * m) {
+                        VD_RARE;
                         if (rdA && __builtin_amdgcn_ballot_w64((V & 0xFFFFu) != (cpv[m] & 0xFFFFu)) == 0) {
                             kmaxA = kmaxA < j ? kmaxA : j;
                             stop = true;
@@ -552,6 +558,7 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(SPL
                         cpv[m] = __builtin_amdgcn_perm(cpv[m], V, 0x07060100u);
                     }
                     if (j == ckB + 3u * m) {
+                        VD_RARE;
                         if (rdB && __builtin_amdgcn_ballot_w64((V >> 16) != (cpv[m] >> 16)) == 0) {
                             kmaxB = kmaxB < j ? kmaxB : j;
                             stop = true;
@@ -563,6 +570,7 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(SPL
                 // vectors are the converged ones, so keeping them changes nothing)
                 if (stop) nblk = (kmaxA > kmaxB ? kmaxA : kmaxB) + 2u;
             }
+#undef VD_RARE
         }
         wave_sync();
         if (j >= 1) {
