@@ -262,8 +262,9 @@ constexpr int kPkWarm = 6;
 constexpr int kPkChk = 2;
 __host__ __device__ constexpr uint32_t pk_cut(uint32_t p, uint32_t P, uint32_t W)
 {
-    // 6 + 3 * round(p (W - 6) / (3 P)) for 0 < p < P
-    return p == 0 ? 0u : p >= P ? W : 6u + 3u * ((2u * p * (W - 6u) + 3u * P) / (6u * P));
+    // kPkWarm + 3 * round(p (W - kPkWarm) / (3 P)) for 0 < p < P (the parts' first blocks minus the warm-up
+    // are multiples of 3 blocks)
+    return p == 0 ? 0u : p >= P ? W : (uint32_t)kPkWarm + 3u * ((2u * p * (W - (uint32_t)kPkWarm) + 3u * P) / (6u * P));
 }
 
 // NW, ABL: tools only (waves per SIMD of the LDS layout; component ablations as vd_decode_tg's, wrong outputs)
