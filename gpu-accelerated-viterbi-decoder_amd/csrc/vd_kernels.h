@@ -158,9 +158,10 @@ struct Fair {
     {
         if (!mine) return;
         if (last != kFairEmpty) {
-            const bool act = lane < kFairWaves && seen != kFairEmpty;
-            const uint32_t n = (uint32_t)__builtin_popcountll(__ballot(act));
-            uint32_t x = act ? seen : 0u;
+            // (no selects: v_cndmask issues in about 18 cycles at 8 waves per SIMD.)  Lanes 0..15 read the 16
+            // words; an empty slot (kFairEmpty = ~0; posted values stay below 2^31) adds 0
+            const uint32_t n = (uint32_t)__builtin_popcountll(__ballot(seen != kFairEmpty) & ((1ull << kFairWaves) - 1ull));
+            uint32_t x = seen & ~(uint32_t)((int32_t)seen >> 31);
             // sum of the 16 words: row_shr 1, 2, 4, 8 (lanes past the row edge add 0); lane 15 holds it
             x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, true);
             x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xF, 0xF, true);
