@@ -156,18 +156,23 @@ N_XCD = 8         # rocprofv3 sums GRBM_GUI_ACTIVE over the 8 XCDs (MI355X_MICRO
 
 
 def acs_only_ms(name):
-    """Instruction-mix ceiling of a workload's kernel: the time per batch of the same batched launch with
-    only the ACS recursion left (tools/vd_pkab 'ACS only' variant: no table build/reads, read-out, loads or
-    traceback; 20 batches per launch), from the committed ablation log of this round; None if absent."""
-    col = {"hard_b32": 0, "soft8_b16": 1}.get(name)
+    """Instruction-mix ceiling of a workload's kernel: (ACS-only ms, full ms) per batch of the same batched
+    launch on one box (tools/vd_pkab: 'ACS only' = no table build/reads, read-out, loads or traceback; 20
+    batches per launch), from the committed ablation log of this round; None if absent.  Boxes differ by up
+    to 15 %, so only the ratio of the two is carried over to the live kernel."""
+    col = {"hard_b32": 0, "soft8_b16": 1, "fp32_f16": 2}.get(name)
     p = os.path.join(ROOT, "profiles", PMC_ROUND, "ablate_batched.log")
     if col is None or not os.path.exists(p):
         return None
+    acs = full = None
     with open(p) as f:
         for line in f:
-            if line.startswith("ACS only"):
-                return float(line.split(")")[-1].split()[col])
-    return None
+            cells = line.split(")")[-1].split() if line.startswith("ACS only") else line.split()[1:]
+            if line.startswith("ACS only") and acs is None:
+                acs = float(cells[col]) if len(cells) > col else None
+            elif line.startswith("full ") and full is None:
+                full = float(cells[col]) if len(cells) > col else None
+    return (acs, full) if acs and full else None
 
 
 def valu_model():
@@ -224,10 +229,13 @@ def valu_view(pmc, kernel_ms, stages, name, msg_bits):
                                 "source": f"profiles/{PMC_ROUND}/valu_model.json (tools/isa_mix.py)"}
             v["cycle_model_pct_live"] = round(100.0 * need / (kernel_ms * 1e-3 * ghz * 1e9), 1)
             v["cycle_model_pct"] = round(100.0 * need / cyc, 1)
-    acs = acs_only_ms(name)
-    if acs:
-        v["mix_ceiling"] = {"acs_only_ms": acs, "gbps": round(msg_bits / (acs * 1e-3) / 1e9, 2),
-                            "frac": round(acs / kernel_ms, 3),
+    ab = acs_only_ms(name)
+    if ab:
+        # the ablation box's ACS-only / full ratio applied to the live kernel time
+        frac = ab[0] / ab[1]
+        v["mix_ceiling"] = {"acs_only_ms": round(frac * kernel_ms, 4),
+                            "gbps": round(msg_bits / (frac * kernel_ms * 1e-3) / 1e9, 2), "frac": round(frac, 3),
+                            "ablation_ms": {"acs_only": ab[0], "full": ab[1]},
                             "source": f"profiles/{PMC_ROUND}/ablate_batched.log (tools/vd_pkab: codeword input, 20 batches per launch)"}
     v["source"] = f"profiles/{PMC_ROUND}/pmc_summary.json"
     return v
