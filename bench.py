@@ -310,6 +310,12 @@ def free_port():
         return s.getsockname()[1]
 
 
+# Rehearsal of the N > 1 path on a 1-GPU box (tests/test_gpu_dist.py): every rank decodes on cuda:0 and the
+# collectives run over gloo on host tensors.  Its numbers are not a measurement (the ranks share one GPU);
+# the line says so in config.parallelism and config.rehearsal.
+REHEARSE = os.environ.get("VD_BENCH_REHEARSE_SHARED_GPU") == "1"
+
+
 def init_ranks(world, local):
     """The process group every run uses, N = 1 included, so the N = 1 point runs the same collectives as
     N > 1 (barrier, max over ranks, checksum gather, final gather): RCCL (backend "nccl") bound to this
@@ -319,6 +325,10 @@ def init_ranks(world, local):
         assert world == 1
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(free_port()), RANK="0", WORLD_SIZE="1",
                           LOCAL_RANK="0")
+    if REHEARSE:
+        torch.cuda.set_device(0)
+        torch.distributed.init_process_group("gloo")
+        return
     torch.cuda.set_device(local)
     torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local))
 
@@ -652,10 +662,11 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if args.ranks_check:
         return ranks_check(world, rank)
-    if torch.cuda.device_count() < world:
+    if torch.cuda.device_count() < world and not REHEARSE:
         sys.exit(f"bench.py: {world} ranks but only {torch.cuda.device_count()} visible GPU(s)")
     init_ranks(world, local)
     dev = torch.cuda.current_device()
+    cdev = "cpu" if REHEARSE else dev  # where the collectives' tensors live
     stream = torch.cuda.current_stream()
     sptr = stream.cuda_stream
 
@@ -729,7 +740,7 @@ def main():
     warm_iteration()
     t_it = time.perf_counter() - tw
     n_more = max(-(-args.warmup // K), int(np.ceil(args.warm_s / max(t_it, 1e-6)))) - 1
-    n_more = int(max_over_ranks(float(n_more), dev))
+    n_more = int(max_over_ranks(float(n_more), cdev))
     for _ in range(n_more):
         warm_iteration()
     nwarm = K * (1 + n_more)
@@ -785,9 +796,9 @@ def main():
     chan = None if (args.no_channel or not side) else channel_side_measurement(dev, sptr)
     pcie = None if (args.no_pcie or not side) else pcie_side_measurement(batches, dev)
     # the same collectives at every N (N = 1: a 1-rank RCCL group)
-    elapsed = max_over_ranks(elapsed, dev)
-    gathered = gather_checksums(sums + sums0, dev, world)
-    gms, gsums, err = gather_outputs([b["out"] for b in batches], dev, world, rank)
+    elapsed = max_over_ranks(elapsed, cdev)
+    gathered = gather_checksums(sums + sums0, cdev, world)
+    gms, gsums, err = gather_outputs([b["out"].cpu() if REHEARSE else b["out"] for b in batches], cdev, world, rank)
     final_gather = None
     if rank == 0:
         if err is not None:  # a side measurement: report it, keep the bench line
@@ -849,7 +860,8 @@ def main():
                             "uses the reference's 6400-chunk partition",
                 "n_bits_per_batch": N_BITS,
                 "decoded_bits_per_batch": batches[0]["msg"],
-                "parallelism": f"batch-shard x{world}" if world > 1 else "single GPU (1-rank RCCL group)",
+                "parallelism": (f"rehearsal: {world} ranks sharing cuda:0, collectives over gloo" if REHEARSE else
+                                f"batch-shard x{world}" if world > 1 else "single GPU (1-rank RCCL group)"),
                 "launch": {"entry": "vd_run_device_batch", "batches_per_launch": P, "launches": len(sizes),
                            "what": "each workload's K steps as one launch of K independent batches (K "
                                    "resident inputs from distinct seeds, every batch's BER checked against its "
@@ -907,6 +919,8 @@ def main():
             result["config"]["final_gather"] = final_gather
         if not metric_run:
             result["config"]["profiling_workloads"] = names
+        if REHEARSE:
+            result["config"]["rehearsal"] = "not a measurement: every rank decodes on the same GPU"
         if checks is not None:
             result["config"]["parity"] = parity_block(checks)
         if not args.no_cpu_baseline and metric_run:  # every N, on rank 0 (the node's own cores)

@@ -46,3 +46,46 @@ def test_rccl_one_rank_collectives_on_cuda_tensors():
     assert d["max"] == 1.25
     assert d["sums"] == [[0xDEAD0001, 0xBEEF0002, 7]]
     assert d["gather"] == [d["want"]] and d["want"][0] != 0
+
+
+def _bench_json(cmd, env):
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout[-3000:]
+    return json.loads(lines[0])
+
+
+@pytest.mark.gpu
+def test_batch_shard_rehearsal_equals_one_rank():
+    """configs[3]'s batch sharding rehearsed on one GPU: 4 ranks (torch.distributed.run), each decoding its own
+    batch on cuda:0 with the collectives over gloo (bench.py REHEARSE), against one rank decoding the same 4
+    batches (seeds: batch i = 2 (rank + world step) + workload).  The per-rank checksums XOR to the one-rank
+    run's, whose parity block checks batches 0 and 3 against the oracle, and the final gather reaches rank 0
+    with every rank's words intact."""
+    import bench
+    flags = ["--warmup", "1", "--warm-s", "0", "--no-cpu-baseline", "--no-llr", "--no-pcie", "--no-channel",
+             "--no-other"]
+    env = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT", "VD_BENCH_REHEARSE_SHARED_GPU"):
+        env.pop(k, None)
+    one = _bench_json([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "4", *flags], env)
+    world = 4
+    shard = _bench_json([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
+                         "--master-addr", "127.0.0.1", "--master-port", str(bench.free_port()),
+                         os.path.join(ROOT, "bench.py"), "--gpus", str(world), "--steps", "1", *flags],
+                        dict(env, VD_BENCH_REHEARSE_SHARED_GPU="1"))
+    assert shard["n_gpus"] == world and shard["config"]["rehearsal"]
+    assert shard["config"]["parallelism"].startswith("rehearsal")
+    assert all(v["mismatches"] == 0 for v in one["config"]["parity"]["paths"].values()), one["config"]["parity"]
+    assert all(v["mismatches"] == 0 for v in shard["config"]["parity"]["paths"].values()), shard["config"]["parity"]
+    cs = [[int(x, 16) for x in r] for r in shard["checksums"]]
+    assert len(cs) == world
+    want = [int(x, 16) for x in one["checksums"][0]]
+    for w in range(len(want)):
+        acc = 0
+        for r in range(world):
+            acc ^= cs[r][w]
+        assert acc == want[w], (w, [hex(c[w]) for c in cs], hex(want[w]))
+    fg = shard["config"]["final_gather"]
+    assert fg["world"] == world and fg["checksums_match"] is True, fg

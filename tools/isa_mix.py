@@ -49,29 +49,31 @@ def compile_isa():
 def blocks_of(asm, sym):
     i = asm.index("\n" + sym + ":")
     body = asm[i:asm.index(".Lfunc_end", i)].split("\n")
-    out, cur, name, hdr = [], [], "entry", False
+    # a block: (label, opcodes, loop header?, inside a loop?) from the compiler's "Loop Header" / "in Loop"
+    # annotations on the label line
+    out, cur, name, hdr, inl = [], [], "entry", False, False
     for line in body:
         st = line.strip()
         m = re.match(r"^(\.LBB\w+|; %bb\.\d+):", st)
         if m:
-            out.append((name, cur, hdr))
-            cur, name, hdr = [], m.group(1), "Loop Header" in st
+            out.append((name, cur, hdr, inl))
+            cur, name, hdr, inl = [], m.group(1), "Loop Header" in st, "Loop" in st
         elif st and not st.startswith((";", ".")):
             cur.append(st.split()[0])
-    out.append((name, cur, hdr))
+    out.append((name, cur, hdr, inl))
     return out
 
 
 def group_mix(blocks):
     """per-group dynamic VALU counts by opcode over the group loop's blocks"""
-    start = next(k for k, (_, _, h) in enumerate(blocks) if h)
-    # the loop ends at the last block that branches back to the header
-    hdr = blocks[start][0]
+    start = next(k for k, b in enumerate(blocks) if b[2])
     mix = Counter()
-    for name, ins, _ in blocks[start:]:
+    for name, ins, _, inl in blocks[start:]:
         c = Counter(ins)
         if "s_endpgm" in c:
             break
+        if not inl:  # after the group loop (the guard check, the split's pass epilogue): once per kernel
+            continue
         if any(op.startswith(("ds_read_u8", "ds_read_u16")) for op in c):
             w = 1.0 / TBS  # a traceback body: one pass per TBS blocks
         elif "s_setprio" in c or "v_add_u32_dpp" in c or "global_load_dword" in c or "global_store_dword" in c:
