@@ -295,6 +295,10 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(SPL
     const void* const in = (const char*)in_all + batch * geo.inStride;
     char* const out = (char*)out_all + batch * geo.outStride;
     const ChunkRange crA = chunk_range(geo, cA), crB = SPL ? crA : chunk_range(geo, cA + 1);
+    // kAblClock (tools/vd_pkclock): s_memrealtime at the start, after the first pass and at the end
+    const uint64_t t_rt0 = (ABL & kAblClock) ? __builtin_amdgcn_s_memrealtime() : 0;
+    uint64_t t_rtp = 0;
+    uint32_t npass = 0;
     if (crA.words == 0 && crB.words == 0) return;
     if (geo.check && lane < 3 * kGuardWords) wlds[LL::guard(lane)] = kGuardPattern;
 
@@ -322,7 +326,7 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(SPL
     // field clear: (V & FNM) | FHF, both halves
     constexpr uint32_t FNM = (0xFFFFu << S & 0xFFFFu) * 65537u, FHF = (1u << (S - 1)) * 65537u;
     Fair fair;
-    fair.begin(batch + 1 < geo.nbatch ? nullptr : geo.fair, lane);
+    fair.begin(batch + 1 < geo.nbatch && !(ABL & kAblFairAll) ? nullptr : geo.fair, lane);
     const uint64_t availB = IN::bytes(geo.availStages);
     const uint32_t vo1 = IN::voff(sA), vo2 = IN::voff(sB);
     // 32-bit words traced per chunk (O_B16: each written as two 16-bit words, vd_decode_tg's policy)
@@ -716,13 +720,20 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(SPL
                 rAB = IN::template load<0>(rsB, vo1);
                 rBB = IN::template load<0>(rsB, vo2);
             }
-            if ((j / 3) % 2 == 0) fair.group(j, 3u, lane);
+            // the fairness controller at every group head (every other: SOFT8 split launches 1.4 % slower,
+            // profiles/r05/split_fairness_ab.log)
+            if constexpr (!(ABL & kAblNoFair))
+                if (!(ABL & kAblFair2) || (j / 3) % 2 == 0) fair.group(j, 3u, lane);
             wave_sync();
             sfor<TGD>([&](auto X) { issue(X); });
             if (!block(std::integral_constant<int, 0>{}, j)) break;
             if (!block(std::integral_constant<int, 2>{}, j + 1)) break;
             if (!block(std::integral_constant<int, 4>{}, j + 2)) break;
             wave_sync();
+        }
+        if constexpr ((ABL & kAblClock) != 0) {
+            if (pass == 0) t_rtp = __builtin_amdgcn_s_memrealtime();
+            npass = pass + 1u;
         }
         if constexpr (!SPL) break;
         // SPL: the left neighbours' end vectors: B's is A's (sv1 low); A's is the previous wave's B end
@@ -828,6 +839,19 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(SPL
         }
     }
     fair.end(lane);
+    if constexpr ((ABL & kAblClock) != 0) {  // 8 words per wave behind the outputs (at least 16 MiB in)
+        const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
+        if (lane == 0) {
+            const uint64_t so = geo.nbatch * geo.outStride > (16u << 20) ? geo.nbatch * geo.outStride : (16u << 20);
+            uint64_t* d = (uint64_t*)((char*)out_all + so) + 8 * (blockIdx.x * kWaves + wv);
+            d[0] = t_rt0;
+            d[1] = t_rtp;
+            d[2] = t1;
+            d[3] = (uint32_t)__builtin_amdgcn_s_getreg(4 | (0 << 6) | (31 << 11));   // HW_ID
+            d[4] = (uint32_t)__builtin_amdgcn_s_getreg(20 | (0 << 6) | (31 << 11));  // XCC_ID
+            d[5] = npass;
+        }
+    }
     if constexpr ((ABL & kAblNoStores) != 0) {
         if (sink == 0x9E3779B9u) ((uint32_t*)out)[lane] = sink;  // keeps the traceback live
     }

@@ -60,6 +60,9 @@ constexpr int kAblNoStores = 524288;
 constexpr int kAblLoad2 = 1048576;
 constexpr int kAblAcsOnly = kAblNoTraceback | kAblNoTabReads | kAblNoReadout | kAblNoTabBuild | kAblNoLoads;
 constexpr int kAblNoLdsX = 2097152;  // vd_decode_pk: the two LDS-exchange stages as DPP stages (wrong outputs)
+// vd_decode_pk fairness studies (tools/vd_pkclock): the controller at every other group head (round 5's form);
+// the controller in every batch of a batched launch
+constexpr int kAblFair2 = 4194304, kAblFairAll = 67108864;
 
 template <int CH>
 struct TgFmt {
