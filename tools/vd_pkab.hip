@@ -1,10 +1,10 @@
 // vd_pkab.hip -- timing-only A/B of vd_decode_pk variants in batched launches (not part of the product): the
 // bench's timed region (K distinct resident 32M-bit batches per launch) for HARD/b32 (K=7 codeword through a
-// BSC, p = 0.04), SOFT8/b16 (BPSK codeword + Gaussian noise at Eb/N0 2 dB, quantised like
+// BSC, p = 0.04 unless given), SOFT8/b16 (BPSK codeword + Gaussian noise at Eb/N0 2 dB, quantised like
 // SoftDecisionPacker(SOFT8)) and FP32/f16 (the same noisy values as floats, BASELINE configs[4]).  Variants alternate round by round with a rotating order; every exact variant's
 // words are compared with variant 0's (last batch).  Component ablations (ABL bits, vd_kernel_tg.h) give
 // wrong words by design and are labelled so.
-// Usage: vd_pkab [rounds] [batches per launch]
+// Usage: vd_pkab [rounds] [batches per launch] [HARD flip probability, default 0.04]
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstdlib>
@@ -43,6 +43,7 @@ static double median(std::vector<float> v)
 int main(int argc, char** argv)
 {
     const int rounds = argc > 1 ? atoi(argv[1]) : 6, K = argc > 2 ? atoi(argv[2]) : 20;
+    const double pbsc = argc > 3 ? atof(argv[3]) : 0.04;  // HARD: flip probability of the binary symmetric channel
     const size_t N = 32000000;  // coded stages per batch (the bench's 32M-bit input)
     std::mt19937 rng(7);
     std::vector<uint8_t> o0(N), o1(N);
@@ -55,7 +56,7 @@ int main(int argc, char** argv)
     std::vector<uint32_t> hh(N / 16 + 64, 0u);
     std::uniform_real_distribution<double> U(0.0, 1.0);
     for (size_t t = 0; t < N; t++) {
-        uint32_t a = o0[t] ^ (U(rng) < 0.04), b = o1[t] ^ (U(rng) < 0.04);
+        uint32_t a = o0[t] ^ (U(rng) < pbsc), b = o1[t] ^ (U(rng) < pbsc);
         hh[t / 16] |= (a << (31 - 2 * (t % 16))) | (b << (30 - 2 * (t % 16)));
     }
     const double sigma = std::sqrt(1.0 / (2.0 * 0.5 * std::pow(10.0, 0.2)));
