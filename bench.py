@@ -923,7 +923,7 @@ def main():
             result["config"]["rehearsal"] = "not a measurement: every rank decodes on the same GPU"
         if checks is not None:
             result["config"]["parity"] = parity_block(checks)
-        if not args.no_cpu_baseline and metric_run:  # every N, on rank 0 (the node's own cores)
+        if not args.no_cpu_baseline and metric_run and world == 1:  # rank 0 at N = 1 only (the bench contract)
             result["cpu_baseline"] = cpu_baseline(batches)
         print(json.dumps(result), flush=True)
 
