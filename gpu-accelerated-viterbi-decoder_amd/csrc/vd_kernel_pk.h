@@ -129,6 +129,8 @@ struct PkLds {
 };
 static_assert(PkLds<8>::TBS == 5 && kWaves * PkLds<8>::WAVE * 4 <= 20480 && PkLds<8>::WAVE % 64 == 0,
               "8 workgroups of 4 waves per CU, ring slots 256-B aligned");
+static_assert(PkLds<7>::TBS == 6 && 7 * kWaves * PkLds<7>::WAVE * 4 <= 163840 && PkLds<7>::WAVE % 64 == 0,
+              "split launches: 7 workgroups of 4 waves per CU");
 
 // SOFT8 traceback of one word (header "Ring and traceback"): A = the lane's emit slot (block k + 1; the
 // convergence block k + 2 is the next slot, +512 B) | 2 for chunk B's half; z[r] = 2 + the position bit of the
@@ -267,8 +269,11 @@ __host__ __device__ constexpr uint32_t pk_cut(uint32_t p, uint32_t P, uint32_t W
     return p == 0 ? 0u : p >= P ? W : (uint32_t)kPkWarm + 3u * ((2u * p * (W - (uint32_t)kPkWarm) + 3u * P) / (6u * P));
 }
 
-// NW, ABL: tools only (waves per SIMD of the LDS layout; component ablations as vd_decode_tg's, wrong outputs)
-template <int CH, int CORE, int OB = 32, bool SPL = false, int NW = 8, int ABL = 0>
+// NW: waves per SIMD the LDS layout is cut for: 8 (batched), 7 for split launches (7 workgroups per CU hold
+// every wave of a single batch, so a wave's 5,632 B leave room for 6 words per traceback pass instead of 5:
+// 1.4-1.6 % faster, profiles/r05/split_fairness_ab.log); ABL: tools only (component ablations as
+// vd_decode_tg's, wrong outputs)
+template <int CH, int CORE, int OB = 32, bool SPL = false, int NW = SPL ? 7 : 8, int ABL = 0>
 __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(SPL ? 7 : NW))) void vd_decode_pk(const void* __restrict__ in_all, void* __restrict__ out_all, Geom geo)
 {
     constexpr bool P2 = PkFmt<CH>::P2;

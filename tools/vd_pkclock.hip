@@ -80,8 +80,8 @@ int main(int argc, char** argv)
     struct Case { const char* name; KFn f; const char* in; size_t istr; bool split; unsigned grid = 0; };
     constexpr int C = vd::kAblClock;
     const Case cases[] = {
-        {"HARD/b32 split", (KFn)vd::vd_decode_pk<vd::HARD, vd::B32, 32, true, 8, C>, bH, strH, true},
-        {"SOFT8/b16 split", (KFn)vd::vd_decode_pk<vd::SOFT8, vd::B16, 32, true, 8, C>, bS, strS, true},
+        {"HARD/b32 split", (KFn)vd::vd_decode_pk<vd::HARD, vd::B32, 32, true, 7, C>, bH, strH, true},
+        {"SOFT8/b16 split", (KFn)vd::vd_decode_pk<vd::SOFT8, vd::B16, 32, true, 7, C>, bS, strS, true},
         {"HARD/b32 batched x20", (KFn)vd::vd_decode_pk<vd::HARD, vd::B32, 32, false, 8, C>, bH, strH, false},
         {"SOFT8/b16 batched x20", (KFn)vd::vd_decode_pk<vd::SOFT8, vd::B16, 32, false, 8, C>, bS, strS, false},
         {"HARD/b32 batched, one generation of 6 WG per CU", (KFn)vd::vd_decode_pk<vd::HARD, vd::B32, 32, false, 8, C>, bH, strH, false, 1536},
@@ -94,8 +94,8 @@ int main(int argc, char** argv)
         {"SOFT8/b16 batched + fairness, one generation of 8 WG per CU", (KFn)vd::vd_decode_pk<vd::SOFT8, vd::B16, 32, false, 8, C | vd::kAblFairAll>, bS, strS, false, 2048},
         {"HARD/b32 batched + fairness x20", (KFn)vd::vd_decode_pk<vd::HARD, vd::B32, 32, false, 8, C | vd::kAblFairAll>, bH, strH, false},
         {"SOFT8/b16 batched, one generation of 8 WG per CU", (KFn)vd::vd_decode_pk<vd::SOFT8, vd::B16, 32, false, 8, C>, bS, strS, false, 2048},
-        {"HARD/b32 split (no stamps)", (KFn)vd::vd_decode_pk<vd::HARD, vd::B32, 32, true, 8, 0>, bH, strH, true},
-        {"SOFT8/b16 split (no stamps)", (KFn)vd::vd_decode_pk<vd::SOFT8, vd::B16, 32, true, 8, 0>, bS, strS, true},
+        {"HARD/b32 split (no stamps)", (KFn)vd::vd_decode_pk<vd::HARD, vd::B32, 32, true, 7, 0>, bH, strH, true},
+        {"SOFT8/b16 split (no stamps)", (KFn)vd::vd_decode_pk<vd::SOFT8, vd::B16, 32, true, 7, 0>, bS, strS, true},
     };
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
@@ -227,12 +227,14 @@ int main(int argc, char** argv)
     // same-box A/B of the fairness controller on split launches (variants alternate round by round)
     struct Ab { const char* name; KFn hard, soft8; };
     const Ab ab[] = {
-        {"fairness controller at every group head (product)", (KFn)vd::vd_decode_pk<vd::HARD, vd::B32, 32, true, 8, 0>,
+        {"product (LDS for 7 waves, fairness at every group head)", (KFn)vd::vd_decode_pk<vd::HARD, vd::B32, 32, true, 7, 0>,
+         (KFn)vd::vd_decode_pk<vd::SOFT8, vd::B16, 32, true, 7, 0>},
+        {"at every other group head (round 5's first form)", (KFn)vd::vd_decode_pk<vd::HARD, vd::B32, 32, true, 7, vd::kAblFair2>,
+         (KFn)vd::vd_decode_pk<vd::SOFT8, vd::B16, 32, true, 7, vd::kAblFair2>},
+        {"no fairness controller", (KFn)vd::vd_decode_pk<vd::HARD, vd::B32, 32, true, 7, vd::kAblNoFair>,
+         (KFn)vd::vd_decode_pk<vd::SOFT8, vd::B16, 32, true, 7, vd::kAblNoFair>},
+        {"LDS laid out for 8 waves per SIMD (5 words per traceback)", (KFn)vd::vd_decode_pk<vd::HARD, vd::B32, 32, true, 8, 0>,
          (KFn)vd::vd_decode_pk<vd::SOFT8, vd::B16, 32, true, 8, 0>},
-        {"at every other group head (round 5's first form)", (KFn)vd::vd_decode_pk<vd::HARD, vd::B32, 32, true, 8, vd::kAblFair2>,
-         (KFn)vd::vd_decode_pk<vd::SOFT8, vd::B16, 32, true, 8, vd::kAblFair2>},
-        {"no fairness controller", (KFn)vd::vd_decode_pk<vd::HARD, vd::B32, 32, true, 8, vd::kAblNoFair>,
-         (KFn)vd::vd_decode_pk<vd::SOFT8, vd::B16, 32, true, 8, vd::kAblNoFair>},
     };
     const int na = sizeof(ab) / sizeof(ab[0]);
     std::vector<std::vector<float>> ah(na), as(na);
