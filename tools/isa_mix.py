@@ -2,8 +2,9 @@
 
 Compiles vd_decode_pk<HARD,B32> and vd_decode_pk<SOFT8,B16> (the bench's headline kernels, batched form)
 to gfx950 assembly and weighs the basic blocks of the 96-stage group loop by how often they run per group:
-the three block bodies (32 stages each) once, the traceback bodies (ds_read_u8 chains) once per TBS = 5
-blocks, the fairness controller's blocks every other group, everything else in the loop once.  Output per
+the three block bodies (32 stages each) once, the traceback bodies (ds_read_u8 chains) once per TBS
+blocks (5 words per pass for HARD, 6 for SOFT8), the fairness controller's blocks every other group,
+everything else in the loop once.  Output per
 kernel: VALU instructions per chunk-stage (a chunk's 64 states for one stage; two chunks per wave), by
 opcode, and the same with per-opcode issue costs from a vd_ubench12 log (cycles, relative to v_fma_f32 at 2
 cycles: MI355X_MICROARCH.md), i.e. the VALU cycles a chunk-stage needs.  bench.py reads the JSON this writes
@@ -22,7 +23,8 @@ from collections import Counter
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(ROOT, "gpu-accelerated-viterbi-decoder_amd", "csrc")
 KERNELS = {"hard_b32": "vd::HARD, vd::B32", "soft8_b16": "vd::SOFT8, vd::B16"}
-TBS = 5
+TBS = 5  # words per traceback pass (PkLds: 5 at 8 waves per SIMD, 6 at 7; set per kernel in main)
+TBS_OF = {"hard_b32": 5, "soft8_b16": 6}
 # ubench12 row name for an opcode (issue cost); opcodes not measured take the 4-cycle class of bit/int ops
 UB = {"v_add_f32": "add_f32", "v_sub_f32": "sub_f32", "v_fma_f32": "fma_f32", "v_max_f32": "max_f32",
       "v_add_u32": "add_u32", "v_sub_u32": "sub_u32", "v_sub_u32_dpp": "sub_u32_dpp", "v_pk_max_u16": "pk_max_u16",
@@ -106,6 +108,8 @@ def main():
     for name, args in KERNELS.items():
         sym = next(s for s in re.findall(r"\n(_ZN2vd12vd_decode_pk\w+):", asm)
                    if s.startswith("_ZN2vd12vd_decode_pkILi%dELi%d" % ((0, 0) if name == "hard_b32" else (2, 1))))
+        global TBS
+        TBS = TBS_OF[name]
         mix = group_mix(blocks_of(asm, sym))
         per = {op: n / (96 * 2) for op, n in mix.items()}  # a group: 96 stages of two chunks
         total = sum(per.values())

@@ -15,21 +15,23 @@
 #include "../gpu-accelerated-viterbi-decoder_amd/csrc/vd_kernel_pk.h"
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP error %s at %d\n", hipGetErrorString(e), __LINE__); exit(1); } } while (0)
 using KFn = void (*)(const void*, void*, vd::Geom);
-template <int CH, int CORE, int ABL, int NW = 8>
-constexpr KFn pk() { return (KFn)vd::vd_decode_pk<CH, CORE, 32, false, NW, ABL>; }
+// NW 0: the product's layout for the format (7 waves per SIMD for SOFT8, 8 otherwise)
+template <int CH, int CORE, int ABL, int NW = 0>
+constexpr KFn pk() { return (KFn)vd::vd_decode_pk<CH, CORE, 32, false, NW ? NW : (vd::PkFmt<CH>::P2 ? 7 : 8), ABL>; }
 struct Variant { const char* name; KFn hard, soft8, fp32; bool exact; };
 #define VD_PKAB_ALL(NAME, ABL, NW, EXACT) \
     {NAME, pk<vd::HARD, vd::B32, ABL, NW>(), pk<vd::SOFT8, vd::B16, ABL, NW>(), pk<vd::FP32, vd::F16, ABL, NW>(), EXACT}
 #ifndef VD_PKAB_VARIANTS
 #define VD_PKAB_VARIANTS                                                                          \
-    VD_PKAB_ALL("full", 0, 8, true), VD_PKAB_ALL("ACS only (ablation)", vd::kAblAcsOnly, 8, false), \
-    VD_PKAB_ALL("-traceback (ablation)", vd::kAblNoTraceback, 8, false),                          \
-    VD_PKAB_ALL("-read-out (ablation)", vd::kAblNoReadout, 8, false),                             \
-    VD_PKAB_ALL("-table build (ablation)", vd::kAblNoTabBuild, 8, false),                         \
-    VD_PKAB_ALL("-table reads (ablation)", vd::kAblNoTabReads, 8, false),                         \
-    VD_PKAB_ALL("-input loads (ablation)", vd::kAblNoLoads, 8, false),                            \
-    VD_PKAB_ALL("LDS exchanges as DPP (ablation)", vd::kAblNoLdsX, 8, false),                     \
-    VD_PKAB_ALL("ACS only, LDS exchanges as DPP", vd::kAblAcsOnly | vd::kAblNoLdsX, 8, false),    \
+    VD_PKAB_ALL("full", 0, 0, true), VD_PKAB_ALL("ACS only (ablation)", vd::kAblAcsOnly, 0, false), \
+    VD_PKAB_ALL("-traceback (ablation)", vd::kAblNoTraceback, 0, false),                          \
+    VD_PKAB_ALL("-read-out (ablation)", vd::kAblNoReadout, 0, false),                             \
+    VD_PKAB_ALL("-table build (ablation)", vd::kAblNoTabBuild, 0, false),                         \
+    VD_PKAB_ALL("-table reads (ablation)", vd::kAblNoTabReads, 0, false),                         \
+    VD_PKAB_ALL("-input loads (ablation)", vd::kAblNoLoads, 0, false),                            \
+    VD_PKAB_ALL("LDS exchanges as DPP (ablation)", vd::kAblNoLdsX, 0, false),                     \
+    VD_PKAB_ALL("ACS only, LDS exchanges as DPP", vd::kAblAcsOnly | vd::kAblNoLdsX, 0, false),    \
+    VD_PKAB_ALL("8 waves/SIMD, 5 words per traceback", 0, 8, true),                                \
     VD_PKAB_ALL("7 waves/SIMD, 6 words per traceback", 0, 7, true),                                \
     VD_PKAB_ALL("6 waves/SIMD, 8 words per traceback", 0, 6, true),
 #endif
