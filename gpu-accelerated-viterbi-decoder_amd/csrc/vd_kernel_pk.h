@@ -271,11 +271,12 @@ __host__ __device__ constexpr uint32_t pk_cut(uint32_t p, uint32_t P, uint32_t W
 
 // NW: waves per SIMD the LDS layout is cut for.  7 for split launches (7 workgroups per CU hold every wave
 // of a single batch, so a wave's 5,632 B leave room for 6 words per traceback pass instead of 5: 1.4-1.6 %
-// faster, profiles/r05/split_fairness_ab.log) and for batched SOFT8 (its heavier stages hide latency with 7
-// waves, and the passes come 5/6 as often: ≈ 1 % faster, profiles/r05/ablate_nw7.log); 8 for the other
-// batched formats (HARD loses ≈ 1 % at 7).  ABL: tools only (component ablations as vd_decode_tg's, wrong
-// outputs)
-template <int CH, int CORE, int OB = 32, bool SPL = false, int NW = (SPL || PkFmt<CH>::P2) ? 7 : 8, int ABL = 0>
+// faster, profiles/r05/split_fairness_ab.log) and for batched SOFT8 and FP32 (their heavier stages hide
+// latency with 7 waves, and the passes come 5/6 as often: 0.5-0.7 % faster against a repeated 8-wave control,
+// profiles/r05/ablate_nw7.log); 8 for batched HARD and SOFT4 (HARD loses 0.6-1.6 % at 7).  ABL: tools only
+// (component ablations as vd_decode_tg's, wrong outputs)
+template <int CH, int CORE, int OB = 32, bool SPL = false, int NW = (SPL || PkFmt<CH>::P2 || (CH & 7) == FP32) ? 7 : 8,
+          int ABL = 0>
 __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(SPL ? 7 : NW))) void vd_decode_pk(const void* __restrict__ in_all, void* __restrict__ out_all, Geom geo)
 {
     constexpr bool P2 = PkFmt<CH>::P2;

@@ -15,9 +15,9 @@
 #include "../gpu-accelerated-viterbi-decoder_amd/csrc/vd_kernel_pk.h"
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP error %s at %d\n", hipGetErrorString(e), __LINE__); exit(1); } } while (0)
 using KFn = void (*)(const void*, void*, vd::Geom);
-// NW 0: the product's layout for the format (7 waves per SIMD for SOFT8, 8 otherwise)
+// NW 0: the product's layout for the format (7 waves per SIMD for SOFT8 and FP32, 8 otherwise)
 template <int CH, int CORE, int ABL, int NW = 0>
-constexpr KFn pk() { return (KFn)vd::vd_decode_pk<CH, CORE, 32, false, NW ? NW : (vd::PkFmt<CH>::P2 ? 7 : 8), ABL>; }
+constexpr KFn pk() { return (KFn)vd::vd_decode_pk<CH, CORE, 32, false, NW ? NW : ((vd::PkFmt<CH>::P2 || (CH & 7) == vd::FP32) ? 7 : 8), ABL>; }
 struct Variant { const char* name; KFn hard, soft8, fp32; bool exact; };
 #define VD_PKAB_ALL(NAME, ABL, NW, EXACT) \
     {NAME, pk<vd::HARD, vd::B32, ABL, NW>(), pk<vd::SOFT8, vd::B16, ABL, NW>(), pk<vd::FP32, vd::F16, ABL, NW>(), EXACT}
