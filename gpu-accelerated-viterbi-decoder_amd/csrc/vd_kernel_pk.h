@@ -31,8 +31,9 @@
 // Batched: the two chunks of a wave are consecutive chunks 2w, 2w+1 of the launch (the same batch: 6400 is
 // even); they decode in lockstep over the longer one's blocks, each emitting only its own words.  LDS per wave
 // (PkLds): [ring | guard | label-region table with the +tag area (TgTabLT<true>) | guard | guard]; 6 ring slots
-// of 512 B (both chunks) in a wave's 5,120 B, so a traceback batch traces 5 words per chunk, both chunks'
-// words in one pass (lanes 0..4 chunk A, lanes 32..36 chunk B).
+// of 512 B (both chunks) in a wave's 5,120 B at 8 waves per SIMD, 7 in 5,632 B at 7 (batched SOFT8 and FP32,
+// split launches), so a traceback batch traces 5 (6) words per chunk, both chunks' words in one pass (lanes
+// 0..4 (0..5) chunk A, lanes 32.. chunk B).
 //
 // Read-out.  Every field clear is (V & ~field) | base as one v_bitop3_b32 (2 cycles; v_and_or_b32 takes 4,
 // profiles/r05/ubench12.log).
