@@ -271,7 +271,9 @@ static int ensure_capacity(vd_decoder* d, size_t inBytes, size_t outBytes)
 //    every word kFairEmpty at rest (the kernels free their slots); concurrent launches sharing it only
 //    perturb issue priorities;
 //  * the segment tables of segment launches (read only; vd_kernel_tg.h "segment launches");
-//  * the re-decode counter of segment launches (vd_split_redecodes).
+//  * the re-decode counter of segment and split launches (vd_split_redecodes) and the split launches'
+//    pass-cap counter (vd_split_cap_exits: waves that stopped re-decoding at the cap with a part still
+//    differing; never expected, and vd_run / vd_run_stream fail when it is non-zero).
 // Segment launches keep their boundary vectors in LDS, so launches on any number of streams share no
 // scratch.  A decoder looks the state up once (vd_create), not per launch.
 struct SegTable {
@@ -298,7 +300,7 @@ static DeviceState* device_state(int device)
         x->nsimd = 4 * cus;
         bool ok = hipMalloc(&x->board, vd::kFairBoardWords * 4) == hipSuccess &&
                   hipMemset(x->board, 0xFF, vd::kFairBoardWords * 4) == hipSuccess &&
-                  hipMalloc(&x->stats, 4) == hipSuccess && hipMemset(x->stats, 0, 4) == hipSuccess;
+                  hipMalloc(&x->stats, 8) == hipSuccess && hipMemset(x->stats, 0, 8) == hipSuccess;
         for (int th = 0; th < 3 && ok; th++) {
             const std::vector<uint32_t> t = vd::seg_table(x->nsimd, th);
             if (t.empty()) continue;
@@ -417,6 +419,16 @@ int vd_split_redecodes(int device, uint64_t* count)
     *count = v;
     return VD_OK;
 }
+int vd_split_cap_exits(int device, uint64_t* count)
+{
+    if (!count) return fail(VD_ERR_ARG, "null argument");
+    DeviceState* x = device_state(device);
+    if (!x) return fail(VD_ERR_DEVICE, "per-device decode state unavailable");
+    uint32_t v = 0;
+    VD_HIP(hipMemcpy(&v, x->stats + 1, 4, hipMemcpyDeviceToHost));
+    *count = v;
+    return VD_OK;
+}
 const char* vd_last_error(void) { return g_err.c_str(); }
 const char* vd_kernel_name(int options) { return kname(options); }
 
@@ -428,6 +440,7 @@ const char* vd_decoder_kernel_name(vd_decoder* d, size_t inputNum, int nbatch, i
     static const char* cores[3] = {"B32", "B16", "F16"};
     const int o = d->options;
     const uint64_t packNum = message_len(o, inputNum) / (size_t)bpp_of(o);
+    if (packNum == 0) return "-";  // launch_decode launches nothing
     const std::string args = std::string(llr ? "LLR+" : "") + chs[ch_of(o)] + "," + cores[met_of(o)] + "," +
                              (out_of(o) ? "O16" : "O32") + ">";
     vd::Geom g;
@@ -516,6 +529,20 @@ int vd_destroy(vd_decoder* d)
     return VD_OK;
 }
 
+// vd_run / vd_run_stream (blocking): a single-batch split launch whose re-decode passes hit their cap with a part
+// still differing (vd_kernel_pk.h "Split"; never expected) fails the call instead of returning wrong words
+static int check_split_cap(const vd_decoder* d, size_t inputNum, bool llr = false)
+{
+    const uint64_t packNum = message_len(d->options, inputNum) / (size_t)bpp_of(d->options);
+    if (packNum == 0 || plan_form(d, packNum, 1, llr) != Form::PkSplit) return VD_OK;
+    uint32_t v = 0;
+    VD_HIP(hipMemcpy(&v, d->ds->stats + 1, 4, hipMemcpyDeviceToHost));
+    if (v)
+        return fail(VD_ERR_DEVICE, "split launch reached its re-decode pass cap with a part still differing (" +
+                                       std::to_string(v) + " waves on this device so far): decoded words may be wrong");
+    return VD_OK;
+}
+
 int vd_run(vd_decoder* d, const void* input_h, void* output_h, size_t inputNum, float* kernel_ms)
 {
     if (!d || !input_h || !output_h) return fail(VD_ERR_ARG, "null argument");
@@ -531,7 +558,7 @@ int vd_run(vd_decoder* d, const void* input_h, void* output_h, size_t inputNum, 
         VD_HIP(hipEventRecord(d->ev1, d->stream));
         VD_HIP(hipStreamSynchronize(d->stream));
         if (kernel_ms) VD_HIP(hipEventElapsedTime(kernel_ms, d->ev0, d->ev1));
-        return VD_OK;
+        return check_split_cap(d, inputNum);
     }
     int rc = ensure_capacity(d, inB, outB + 16);
     if (rc != VD_OK) return rc;
@@ -543,7 +570,7 @@ int vd_run(vd_decoder* d, const void* input_h, void* output_h, size_t inputNum, 
     VD_HIP(hipMemcpyAsync(output_h, d->out_d, outB, hipMemcpyDeviceToHost, d->stream));
     VD_HIP(hipStreamSynchronize(d->stream));
     if (kernel_ms) VD_HIP(hipEventElapsedTime(kernel_ms, d->ev0, d->ev1));
-    return VD_OK;
+    return check_split_cap(d, inputNum);
 }
 
 int vd_set_guard_check(vd_decoder* d, int enable)
@@ -672,7 +699,7 @@ int vd_run_llr(vd_decoder* d, const float* llr_h, void* output_h, size_t inputNu
     VD_HIP(hipMemcpyAsync(output_h, d->out_d, outB, hipMemcpyDeviceToHost, d->stream));
     VD_HIP(hipStreamSynchronize(d->stream));
     if (kernel_ms) VD_HIP(hipEventElapsedTime(kernel_ms, d->ev0, d->ev1));
-    return VD_OK;
+    return check_split_cap(d, inputNum, true);
 }
 
 void* vd_host_alloc(size_t bytes)
@@ -713,7 +740,7 @@ int vd_run_stream(vd_decoder* d, const void* const* input_h, void* const* output
         VD_HIP(hipStreamSynchronize(d->stream));
         if (wall_ms)
             *wall_ms = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t0).count();
-        return VD_OK;
+        return nbatches > 0 ? check_split_cap(d, inputNum) : VD_OK;
     }
     int rc = ensure_capacity(d, inB, outB + 16);
     if (rc != VD_OK) return rc;
@@ -783,7 +810,7 @@ int vd_run_stream(vd_decoder* d, const void* const* input_h, void* const* output
     if (rc != VD_OK) return rc;
     if (e1 != hipSuccess || e2 != hipSuccess || e3 != hipSuccess) return fail(VD_ERR_DEVICE, "pipeline failed");
     if (wall_ms) *wall_ms = std::chrono::duration<float, std::milli>(t1 - t0).count();
-    return VD_OK;
+    return nbatches > 0 ? check_split_cap(d, inputNum) : VD_OK;
 }
 
 int vd_run_batches(int options, const void* const* input_h, void* const* output_h, size_t inputNum,

@@ -758,7 +758,13 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(SPL
         const bool mA = pA > 0 && __builtin_amdgcn_ballot_w64((sv2 & 0xFFFFu) != (nb >> 16)) != 0;
         const bool mB = __builtin_amdgcn_ballot_w64((sv1 >> 16) != (sv1 & 0xFFFFu)) != 0;
         const bool more = tail ? __syncthreads_or(mA || mB) != 0 : (mA || mB);
-        if (!more || pass + 1u >= 2u * P) break;  // WG-uniform; after P passes no start differs
+        if (!more) break;  // WG-uniform
+        if (pass + 1u >= 2u * P) {
+            // after P passes no start differs (header), so this cap never binds; if it ever did, the words
+            // of the parts still differing would be wrong: count it (geo.stats[1]) so vd_run fails loudly
+            if (lane == 0 && geo.stats && (mA || mB)) atomicAdd(geo.stats + 1, 1u);
+            break;
+        }
         if (lane == 0 && geo.stats && (mA || mB)) atomicAdd(geo.stats, (mA ? 1u : 0u) + (mB ? 1u : 0u));
         // decode again every part whose start vector differs, from block cut(p) with the left end vector;
         // an idle half repeats the other half's job without writing or keeping vectors

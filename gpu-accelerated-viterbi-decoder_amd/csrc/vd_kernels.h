@@ -46,7 +46,9 @@ struct Geom {
     // kWaves segments (their boundary vectors stay in the workgroup's LDS); null = one chunk per wave
     const uint32_t* seg = nullptr;
     uint32_t segWarm = 6;        // warm-up blocks of a segment that starts inside a chunk (a multiple of 3)
-    uint32_t* stats = nullptr;   // count of segments re-decoded (or null)
+    // [0]: count of segments / parts re-decoded; [1]: split waves that reached the re-decode pass cap with
+    // a part still differing (never expected; vd_run fails when it is non-zero); or null
+    uint32_t* stats = nullptr;
     // LDS guard check (tests): non-null = write guard words around every wave's table and ring and count
     // the ones found overwritten at kernel exit into *check
     uint32_t* check = nullptr;

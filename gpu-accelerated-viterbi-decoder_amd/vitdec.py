@@ -45,7 +45,7 @@ EXPORTS = ["vd_options_valid", "vd_input_size", "vd_message_len", "vd_output_siz
            "vd_simulate_host", "vd_count_errors", "vd_last_error", "vd_device_count", "vd_kernel_name",
            "vd_pack_device", "vd_run_device_llr", "vd_run_llr", "vd_host_alloc", "vd_host_free",
            "vd_run_stream", "vd_channel_device", "vd_simulate_device", "vd_mt_state_after", "vd_split_redecodes",
-           "vd_set_guard_check", "vd_guard_violations", "vd_run_device_llr_batch", "vd_build_info",
+           "vd_split_cap_exits", "vd_set_guard_check", "vd_guard_violations", "vd_run_device_llr_batch", "vd_build_info",
            "vd_decoder_kernel_name"]
 
 
@@ -86,6 +86,7 @@ def lib():
            "vd_simulate_device": ([i, sz, f, ctypes.c_uint32, ctypes.c_uint32, vp, vp, vp], None),
            "vd_mt_state_after": ([ctypes.c_uint32, ctypes.c_uint64, vp], None),
            "vd_split_redecodes": ([i, ctypes.POINTER(ctypes.c_uint64)], None),
+           "vd_split_cap_exits": ([i, ctypes.POINTER(ctypes.c_uint64)], None),
            "vd_set_guard_check": ([vp, i], None), "vd_guard_violations": ([vp, ctypes.POINTER(ctypes.c_uint64)], None),
            "vd_count_errors": ([i, vp, sz, vp, sz], ctypes.c_longlong), "vd_last_error": (None, ctypes.c_char_p),
            "vd_pack_device": ([i, vp, sz, f, vp, vp], None), "vd_host_alloc": ([sz], vp), "vd_host_free": ([vp], None),
@@ -345,6 +346,14 @@ def split_redecodes(device=0):
     """split chunks re-decoded whole on a device so far (a speculative piece start did not converge)"""
     v = ctypes.c_uint64(0)
     _check(lib().vd_split_redecodes(device, ctypes.byref(v)))
+    return v.value
+
+
+def split_cap_exits(device=0):
+    """split-launch waves that stopped re-decoding at the pass cap with a part still differing (always 0: the
+    passes provably end within P; run / run_llr / run_stream raise if it is ever not)"""
+    v = ctypes.c_uint64(0)
+    _check(lib().vd_split_cap_exits(device, ctypes.byref(v)))
     return v.value
 
 

@@ -159,6 +159,12 @@ long long vd_count_errors(int options, const uint8_t* bits, size_t N, const void
  * speculative start had not converged at the boundary (all launches so far; decoded words are exact either
  * way).  VD_NO_SPLIT=1 in the environment (read at vd_create) disables splitting. */
 int vd_split_redecodes(int device, uint64_t* count);
+/* split launches (vd_decode_pk, single batches): waves on a device whose re-decode passes stopped at their cap
+ * (2 P passes for P parts) with a part still differing.  The passes provably end within P (vd_kernel_pk.h
+ * "Split"), so this stays 0; if it ever is not, the words of that launch may be wrong, and the blocking entry
+ * points (vd_run, vd_run_llr, vd_run_stream) return VD_ERR_DEVICE after such a launch.  Callers of the
+ * device-pointer entry points may check it after synchronising. */
+int vd_split_cap_exits(int device, uint64_t* count);
 /* LDS guard check (tests): enable != 0 makes every later launch of this decoder write guard words around
  * each wave's branch-metric table and survivor ring in LDS and count, at kernel exit, the guard words
  * found overwritten (an out-of-bounds LDS store); the count restarts at 0.  Off by default (one uniform
@@ -172,7 +178,8 @@ int vd_device_count(void);
 const char* vd_kernel_name(int options);
 /* the kernel and launch form this decoder takes for a decode of inputNum encoded values in nbatch batches
  * (vd_run_device: nbatch 1; vd_run_device_batch: nbatch) of packed (llr 0) or float (llr 1) input, under
- * the knobs read at vd_create (VD_NO_PK, VD_PK_SPLIT, VD_NO_SPLIT); valid until the thread's next call */
+ * the knobs read at vd_create (VD_NO_PK, VD_PK_SPLIT, VD_NO_SPLIT); "-" when such a decode launches
+ * nothing (fewer than one output word); valid until the thread's next call */
 const char* vd_decoder_kernel_name(vd_decoder* dec, size_t inputNum, int nbatch, int llr);
 /* build record: "<16 hex digits of the SHA-256 of the concatenated sources> <their paths, relative to the
  * package directory>"; the Python binding refuses a library whose sources have changed since (stale build) */

@@ -160,11 +160,13 @@ def test_fused_llr_batch_equals_single(gpu, vd, vo, opt):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("opt", [HARD | M_B32, SOFT4 | M_B16, FP32 | M_FP16, HARD | M_B16 | O_B16], ids=name)
+@pytest.mark.parametrize("opt", [HARD | M_B32, SOFT4 | M_B16, FP32 | M_FP16, HARD | M_B16 | O_B16, SOFT8 | M_B16,
+                                 SOFT8 | M_B32 | O_B16], ids=name)
 def test_fused_llr_split_launch_on_packed_kernel(gpu, vd, vo, opt):
-    """16M bits of float channel values in one fused launch: 78 words per chunk, so HARD / SOFT4 / FP32 run
-    vd_decode_pk's split launch (tail workgroups included) with the packer fused into the table build; equal
-    to the oracle's pack + decode and to the unfused vd_decode_tg path (VD_NO_PK=1)"""
+    """16M bits of float channel values in one fused launch: 78 words per chunk, so HARD / SOFT4 / SOFT8 / FP32
+    run vd_decode_pk's split launch (tail workgroups included) with the packer fused into the table build
+    (SOFT8 with M_B32's tie-tag complement and 16-bit output words too); equal to the oracle's pack + decode and
+    to the unfused vd_decode_tg path (VD_NO_PK=1)"""
     import os
     vals = channel_values_fast(2 * 16_000_000, 1.0, 13)
     packed = vo.pack(opt, vals, 40000.0)
@@ -181,3 +183,24 @@ def test_fused_llr_split_launch_on_packed_kernel(gpu, vd, vo, opt):
     bad = np.flatnonzero(out != ref)
     assert bad.size == 0, f"{bad.size} words differ, first at {bad[:5]}"
     assert np.array_equal(tg, ref)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("opt", [SOFT8 | M_B16, SOFT8 | M_B32 | O_B16, HARD | M_B32], ids=name)
+def test_fused_llr_split_random_floats_redecode(gpu, vd, vo, opt):
+    """Float channel values that carry no codeword (standard normal noise, scaled so the quantiser spans its
+    range): the split launch's speculative starts often do not converge, so the fused float-input kernel's
+    re-decodes and early stops run (vd_split_redecodes grows), the words still equal the oracle's pack +
+    decode, and no wave reaches the pass cap"""
+    vals = (np.random.default_rng(17).standard_normal(2 * 16_000_000) * 2e-3).astype(np.float32)
+    packed = vo.pack(opt, vals, 40000.0)
+    ref, ok = vo.decode(opt, packed, input_num=vals.size, nthreads=16)
+    before, caps = vd.split_redecodes(), vd.split_cap_exits()
+    with vd.ViterbiCUDA(opt) as d:
+        assert "split" in d.kernel_for(vals.size, 1, True)
+        out, _ = d.run_llr(vals, scale=40000.0)
+    redec = vd.split_redecodes() - before
+    bad = np.flatnonzero(out != ref)
+    assert bad.size == 0, f"{bad.size} words differ (re-decoded {redec}), first at {bad[:5]}"
+    assert redec > 0, redec
+    assert vd.split_cap_exits() == caps == 0

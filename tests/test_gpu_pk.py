@@ -127,16 +127,19 @@ def test_packed_split_random_input_redecodes(gpu, vo, opt):
     """Uniformly random channel words: the second part's speculative start often does not converge (HARD:
     652 of 6400 chunks on the first run; SOFT8 about a fifth of the parts), so re-decodes run -- most of them
     stopping at a checkpoint one or two groups after the cut (vd_kernel_pk.h "Early stop"), the rest decoding
-    the whole part -- and the words still equal the oracle's."""
+    the whole part -- and the words still equal the oracle's.  No wave reaches the re-decode pass cap with a
+    part still differing (vd_split_cap_exits: the passes provably end within P, P = 2 per whole-chunk wave and
+    8 per tail workgroup; tests/test_split_model.py checks that bound on the host model)."""
     nbits = 16_000_000
     n = 2 * nbits
     env = {}
     nin = gpu.lib().vd_input_size(opt, n)
     g = torch.Generator(device="cpu").manual_seed(5)
     packed = torch.randint(0, 256, (nin + 256,), dtype=torch.uint8, generator=g).to("cuda")
-    before = gpu.split_redecodes()
+    before, caps = gpu.split_redecodes(), gpu.split_cap_exits()
     pk = _single(gpu, opt, packed, nin, n, env)
     redec = gpu.split_redecodes() - before
+    assert gpu.split_cap_exits() == caps == 0
     p = packed[:nin].cpu().numpy().view(np.int32)
     ref, ok = vo.decode(opt, p, input_num=n, nthreads=16)
     got = pk.cpu().numpy().view(ref.dtype)
@@ -185,8 +188,9 @@ def _soft8_pattern(kind, nin, seed):
 def test_packed_soft8_extreme_inputs(gpu, vo, opt, kind):
     """SOFT8 on vd_decode_pk: batched launches (3 batches) of synthetic channel bytes at the ends of the metric
     range (header of vd_kernel_pk.h: candidates within [-3072, 4864] units of position 0's metric, renormalised
-    every 8 stages), equal to the oracle word for word; the single-batch launch of batch 0 (vd_decode_tg's
-    segment launch: SOFT8 single batches do not run the packed split kernel) too"""
+    every 8 stages), equal to the oracle word for word; the single-batch launch of batch 0 too, both on the
+    packed split kernel (the default for SOFT8 single batches) and on vd_decode_tg's segment launch
+    (VD_PK_SPLIT=0)"""
     nbits = 13_107_264
     n = 2 * nbits
     nb = 3
@@ -198,6 +202,8 @@ def test_packed_soft8_extreme_inputs(gpu, vo, opt, kind):
     packed = host.to("cuda")
     pk, ostride, nout = _decode_batched(gpu, opt, packed, stride, n, nb, no_pk=False)
     single = _single(gpu, opt, packed[:stride], nin, n, {})
+    single_tg = _single(gpu, opt, packed[:stride], nin, n, {"VD_PK_SPLIT": "0"})
+    assert torch.equal(single, single_tg)
     for b in range(nb):
         p = host[b * stride:b * stride + nin].numpy().view(np.int32)
         ref, ok = vo.decode(opt, p, input_num=n, nthreads=16)

@@ -4,7 +4,8 @@
 # through the LDS guard check to show the check catches that bug.  Output: tools/build/scc_scratch/lib/,
 # with BUILD_RECORD: the product's build-record line (vd_build_info format: hash of the product sources the
 # scratch copy was made from, then their paths) -- the test refuses a scratch library whose record no longer
-# matches the tree (vitdec.build_mismatch), so a stale build is never loaded.
+# matches the tree (vitdec.build_mismatch), so a stale build is never loaded; SCC_EVIDENCE: the count of SCC
+# readers after a renormalisation in the scratch ISA.
 set -euo pipefail
 HERE=$(cd "$(dirname "$0")" && pwd)
 ROOT=$(dirname "$HERE")
@@ -29,7 +30,19 @@ cd "$B/pkg"
 $H $F -c csrc/vd_capi.hip -o "$B/vd_capi.o" & p1=$!
 $H $F -c csrc/vd_host.cpp -o "$B/vd_host.o" & p2=$!
 $H $F -c csrc/vd_mtjump.cpp -o "$B/vd_mtjump.o" & p3=$!
-wait $p1 && wait $p2 && wait $p3
+# ISA evidence: SCC readers after a renormalisation in the scratch copy's compiled tg kernels
+# (tests/test_asm_lint.py's scan).  Whether the bug shows at run time depends on the compiler keeping SCC
+# live across the un-clobbered asm; the guard test asserts violations only when this count is non-zero.
+python3 - "$ROOT" "$B/pkg/csrc" "$B/SCC_EVIDENCE" <<'PY' & p4=$!
+import os, sys, tempfile
+sys.path.insert(0, os.path.join(sys.argv[1], "tests"))
+import test_asm_lint as t
+with tempfile.TemporaryDirectory() as d:
+    r = t.scc_reads_after_renorm(t._compile(sys.argv[2], d))
+open(sys.argv[3], "w").write(f"{sum(r.values())}\n")
+PY
+wait $p1 && wait $p2 && wait $p3 && wait $p4
 $H --offload-arch=gfx950 -shared -o "$B/lib/libvitdec.so" "$B/vd_capi.o" "$B/vd_host.o" "$B/vd_mtjump.o"
+mv "$B/SCC_EVIDENCE" "$B/lib/SCC_EVIDENCE"
 echo "$REC" > "$B/lib/BUILD_RECORD"
 echo "built $B/lib/libvitdec.so ($REC)"
