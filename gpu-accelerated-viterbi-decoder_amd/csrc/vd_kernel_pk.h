@@ -274,10 +274,8 @@ __host__ __device__ constexpr uint32_t pk_cut(uint32_t p, uint32_t P, uint32_t W
 // of a single batch, so a wave's 5,632 B leave room for 6 words per traceback pass instead of 5: 1.4-1.6 %
 // faster, profiles/r05/split_fairness_ab.log) and for batched SOFT8 and FP32 (their heavier stages hide
 // latency with 7 waves, and the passes come 5/6 as often: 0.5-0.7 % faster against a repeated 8-wave control,
-// profiles/r05/ablate_nw7.log); 8 for batched HARD and SOFT4 (HARD loses 0.6-1.6 % at 7).  ABL: tools only
-// (component ablations as vd_decode_tg's, wrong outputs)
-template <int CH, int CORE, int OB = 32, bool SPL = false, int NW = (SPL || PkFmt<CH>::P2 || (CH & 7) == FP32) ? 7 : 8,
-          int ABL = 0>
+// profiles/r05/ablate_nw7.log); 8 for batched HARD and SOFT4 (HARD loses 0.6-1.6 % at 7).
+template <int CH, int CORE, int OB = 32, bool SPL = false, int NW = (SPL || PkFmt<CH>::P2 || (CH & 7) == FP32) ? 7 : 8>
 __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(SPL ? 7 : NW))) void vd_decode_pk(const void* __restrict__ in_all, void* __restrict__ out_all, Geom geo)
 {
     constexpr bool P2 = PkFmt<CH>::P2;
@@ -304,10 +302,6 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(SPL
     const void* const in = (const char*)in_all + batch * geo.inStride;
     char* const out = (char*)out_all + batch * geo.outStride;
     const ChunkRange crA = chunk_range(geo, cA), crB = SPL ? crA : chunk_range(geo, cA + 1);
-    // kAblClock (tools/vd_pkclock): s_memrealtime at the start, after the first pass and at the end
-    const uint64_t t_rt0 = (ABL & kAblClock) ? __builtin_amdgcn_s_memrealtime() : 0;
-    uint64_t t_rtp = 0;
-    uint32_t npass = 0;
     if (crA.words == 0 && crB.words == 0) return;
     if (geo.check && lane < 3 * kGuardWords) wlds[LL::guard(lane)] = kGuardPattern;
 
@@ -335,7 +329,7 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(SPL
     // field clear: (V & FNM) | FHF, both halves
     constexpr uint32_t FNM = (0xFFFFu << S & 0xFFFFu) * 65537u, FHF = (1u << (S - 1)) * 65537u;
     Fair fair;
-    fair.begin(batch + 1 < geo.nbatch && !(ABL & kAblFairAll) ? nullptr : geo.fair, lane);
+    fair.begin(batch + 1 < geo.nbatch ? nullptr : geo.fair, lane);
     const uint64_t availB = IN::bytes(geo.availStages);
     const uint32_t vo1 = IN::voff(sA), vo2 = IN::voff(sB);
     // 32-bit words traced per chunk (O_B16: each written as two 16-bit words, vd_decode_tg's policy)
@@ -376,21 +370,10 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(SPL
     uint32_t sv1 = 0, sv2 = 0;
     uint32_t cpv[kPkChk > 0 ? kPkChk : 1] = {};
     uint32_t kb = 0;
-    uint32_t sink = 0;  // kAblNoStores
     uint32_t tbn = LL::TBS - (blockIdx.x & 3u) % LL::TBS;  // staggered first traceback batches
     __amdgpu_buffer_rsrc_t rsA = tg_rsrc<CH>(in, startA, availB), rsB = tg_rsrc<CH>(in, startB, availB);
     typename IN::raw_t rAA = IN::template load<0>(rsA, vo1), rBA = IN::template load<0>(rsA, vo2);
     typename IN::raw_t rAB = IN::template load<0>(rsB, vo1), rBB = IN::template load<0>(rsB, vo2);
-    // kAblLoad2: the next group's words too (loads two groups ahead)
-    constexpr bool LD2 = (ABL & kAblLoad2) != 0;
-    typename IN::raw_t nAA{}, nBA{}, nAB{}, nBB{};
-    if constexpr (LD2) {
-        const __amdgpu_buffer_rsrc_t qA = tg_rsrc<CH>(in, startA + 96ull, availB), qB = tg_rsrc<CH>(in, startB + 96ull, availB);
-        nAA = IN::template load<0>(qA, vo1);
-        nBA = IN::template load<0>(qA, vo2);
-        nAB = IN::template load<0>(qB, vo1);
-        nBB = IN::template load<0>(qB, vo2);
-    }
     // traceback roles: lanes 0..31 trace half A's words, 32..63 half B's
     const bool tbB = lane >= 32;
     const uint32_t tbl = (uint32_t)(lane & 31);
@@ -419,7 +402,7 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(SPL
     auto issue = [&](auto Rc) {
         constexpr int r = decltype(Rc)::value;
         constexpr int K = r % 6;
-        if constexpr ((r / 6) % 2 == 0 && !(ABL & kAblNoTabReads)) vp[r] = *(lptr)(tl + aK[K] + TT::row(r));
+        if constexpr ((r / 6) % 2 == 0) vp[r] = *(lptr)(tl + aK[K] + TT::row(r));
     };
     auto block = [&](auto PHc, uint32_t j) {
         constexpr int PH = decltype(PHc)::value;
@@ -436,15 +419,15 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(SPL
             constexpr int r = 32 * BB + i;
             constexpr bool ODD = (r / 6) % 2 == 1;
             constexpr int RP = ODD ? r - 6 : r;
-            const uint32_t m = (ABL & kAblNoTabReads) ? (uint32_t)aK[K] : ODD ? vp[RP].y : vp[RP].x;
+            const uint32_t m = ODD ? vp[RP].y : vp[RP].x;
             // (the xor-8 and xor-7 stages through ds_swizzle too, 8 cycles of VALU instead of 10: +0.6 % / +5.5 %
             // per HARD batch, the LDS pipe being the other busy resource: profiles/r05/abx_lds_exchanges.log)
-            if constexpr (Q <= 3 || (ABL & kAblNoLdsX)) pk_stage_dpp<(Q <= 3 ? Q : 0)>(V, m);
+            if constexpr (Q <= 3) pk_stage_dpp<Q>(V, m);
             else if constexpr (Q == 4) pk_stage_lds_pre<0x401F>(V, m, pa5);
             else if constexpr (ALT) pk_stage_lds_post(V, m, pa5);
             else pk_stage_lds_pre<0>(V, m, pa5);
             if constexpr (r + TGD < 96) issue(std::integral_constant<int, r + TGD>{});
-            if constexpr (i % J == J - 1 && !(ABL & kAblNoReadout)) {
+            if constexpr (i % J == J - 1) {
                 // field read-out, both chunks, then both fields cleared; renormalisation on the whole word
                 // (vd_decode_tg) every RN stages
                 constexpr int g = (i % 32) / J;
@@ -595,7 +578,7 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(SPL
             wave_sync();
             const uint32_t nw = j - 1 - kb;
             const uint32_t k = kb + tbl;
-            if (!(ABL & kAblNoTraceback) && tbl < nw && k >= (tbB ? kminB : kminA) && k < (tbB ? kmaxB : kmaxA)) {
+            if (tbl < nw && k >= (tbB ? kminB : kminA) && k < (tbB ? kmaxB : kmaxA)) {
                 uint32_t w;
                 const uint32_t r3 = kb % 3u;  // wave-uniform
                 const uint32_t PA = rot3(phA, r3);
@@ -623,9 +606,7 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(SPL
                     w = pk4_traceback<CORE>(tbA2, sft, m5);
                 }
                 const uint32_t kc = k + (tbB ? oB : oA);  // chunk word
-                if constexpr (ABL & kAblNoStores) {
-                    sink ^= w + kc;
-                } else if constexpr (OB == 32) {
+                if constexpr (OB == 32) {
                     ((uint32_t*)out)[tbStart + kc] = w;
                 } else {
                     uint16_t* const o = (uint16_t*)out + tbStart;
@@ -706,22 +687,9 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(SPL
     using P1 = std::integral_constant<int, 1>;
     for (uint32_t pass = 0;; pass++) {
         for (uint32_t j = 0; nblk; j += 3) {
-            if constexpr (!(ABL & kAblNoTabBuild)) {
-                put_row(P0{}, rAA, rAB, sA, r6a);
-                if (lane < 32) put_row(P1{}, rBA, rBB, sB, r6b);
-            }
-            if constexpr (LD2) {
-                rAA = nAA;
-                rBA = nBA;
-                rAB = nAB;
-                rBB = nBB;
-                rsA = tg_rsrc<CH>(in, startA + 32ull * (j + 6), availB);
-                rsB = tg_rsrc<CH>(in, startB + 32ull * (j + 6), availB);
-                nAA = IN::template load<0>(rsA, vo1);
-                nBA = IN::template load<0>(rsA, vo2);
-                nAB = IN::template load<0>(rsB, vo1);
-                nBB = IN::template load<0>(rsB, vo2);
-            } else if constexpr (!(ABL & kAblNoLoads)) {
+            put_row(P0{}, rAA, rAB, sA, r6a);
+            if (lane < 32) put_row(P1{}, rBA, rBB, sB, r6b);
+            {  // the next group's input words
                 rsA = tg_rsrc<CH>(in, startA + 32ull * (j + 3), availB);
                 rsB = tg_rsrc<CH>(in, startB + 32ull * (j + 3), availB);
                 rAA = IN::template load<0>(rsA, vo1);
@@ -731,18 +699,13 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(SPL
             }
             // the fairness controller at every group head (every other: SOFT8 split launches 1.4 % slower,
             // profiles/r05/split_fairness_ab.log)
-            if constexpr (!(ABL & kAblNoFair))
-                if (!(ABL & kAblFair2) || (j / 3) % 2 == 0) fair.group(j, 3u, lane);
+            fair.group(j, 3u, lane);
             wave_sync();
             sfor<TGD>([&](auto X) { issue(X); });
             if (!block(std::integral_constant<int, 0>{}, j)) break;
             if (!block(std::integral_constant<int, 2>{}, j + 1)) break;
             if (!block(std::integral_constant<int, 4>{}, j + 2)) break;
             wave_sync();
-        }
-        if constexpr ((ABL & kAblClock) != 0) {
-            if (pass == 0) t_rtp = __builtin_amdgcn_s_memrealtime();
-            npass = pass + 1u;
         }
         if constexpr (!SPL) break;
         // SPL: the left neighbours' end vectors: B's is A's (sv1 low); A's is the previous wave's B end
@@ -845,31 +808,8 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(SPL
         rBA = IN::template load<0>(rsA, vo2);
         rAB = IN::template load<0>(rsB, vo1);
         rBB = IN::template load<0>(rsB, vo2);
-        if constexpr (LD2) {
-            const __amdgpu_buffer_rsrc_t qA = tg_rsrc<CH>(in, startA + 96ull, availB), qB = tg_rsrc<CH>(in, startB + 96ull, availB);
-            nAA = IN::template load<0>(qA, vo1);
-            nBA = IN::template load<0>(qA, vo2);
-            nAB = IN::template load<0>(qB, vo1);
-            nBB = IN::template load<0>(qB, vo2);
-        }
     }
     fair.end(lane);
-    if constexpr ((ABL & kAblClock) != 0) {  // 8 words per wave behind the outputs (at least 16 MiB in)
-        const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
-        if (lane == 0) {
-            const uint64_t so = geo.nbatch * geo.outStride > (16u << 20) ? geo.nbatch * geo.outStride : (16u << 20);
-            uint64_t* d = (uint64_t*)((char*)out_all + so) + 8 * (blockIdx.x * kWaves + wv);
-            d[0] = t_rt0;
-            d[1] = t_rtp;
-            d[2] = t1;
-            d[3] = (uint32_t)__builtin_amdgcn_s_getreg(4 | (0 << 6) | (31 << 11));   // HW_ID
-            d[4] = (uint32_t)__builtin_amdgcn_s_getreg(20 | (0 << 6) | (31 << 11));  // XCC_ID
-            d[5] = npass;
-        }
-    }
-    if constexpr ((ABL & kAblNoStores) != 0) {
-        if (sink == 0x9E3779B9u) ((uint32_t*)out)[lane] = sink;  // keeps the traceback live
-    }
     if (geo.check) {
         wave_sync();
         const bool bad = lane < 3 * kGuardWords && wlds[LL::guard(lane)] != kGuardPattern;

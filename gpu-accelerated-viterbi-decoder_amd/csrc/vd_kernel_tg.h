@@ -40,29 +40,6 @@ namespace vd {
 // channel ids: HARD..FP32 = packed input (viterbiBM.cuh formats); 8 + base = float channel values
 // quantised on the fly exactly like SoftDecisionPacker(base, scale) would have packed them (vd_pack.h)
 constexpr int kLlr = 8;
-// Component ablations (tools/vd_ablate only; the outputs are wrong): the template argument ABL of
-// vd_decode_tg is a set of these bits, 0 in the product.
-constexpr int kAblNoTraceback = 1, kAblNoTabReads = 2, kAblNoReadout = 4, kAblNoTabBuild = 8, kAblNoLoads = 16,
-              kAblClock = 32, kAblNoFair = 256, kAblNoTabWrites = 512;
-// layout variant (tools A/B; an exact twin of the product)
-constexpr int kAblPostExchange = 8192;  // LDS-exchange stages exchange V and subtract after (round 2)
-// exchange variants (exact twins): the xor-32 / xor-16 stage by a VALU lane swap (v_permlane32_swap /
-// v_permlane16_swap) instead of the LDS crossbar: more VALU issue, no LDS round trip in the chain
-constexpr int kAblX32Perm = 16384, kAblX16Perm = 32768;
-// max on the integer patterns (v_max_u32: the metrics are positive normal floats of one binade, so the
-// integer order is the float order): an exact twin
-constexpr int kAblIntMax = 65536;
-// latency studies (tools): table reads 8 stages ahead instead of 4; fairness controller every 4th group head
-constexpr int kAblTgd8 = 131072, kAblFair4 = 262144;
-// vd_decode_pk study: trace back but keep the words in a register (no output stores)
-constexpr int kAblNoStores = 524288;
-// vd_decode_pk study: input loads two groups ahead (a second register set) instead of one
-constexpr int kAblLoad2 = 1048576;
-constexpr int kAblAcsOnly = kAblNoTraceback | kAblNoTabReads | kAblNoReadout | kAblNoTabBuild | kAblNoLoads;
-constexpr int kAblNoLdsX = 2097152;  // vd_decode_pk: the two LDS-exchange stages as DPP stages (wrong outputs)
-// vd_decode_pk fairness studies (tools/vd_pkclock): the controller at every other group head (round 5's form);
-// the controller in every batch of a batched launch
-constexpr int kAblFair2 = 4194304, kAblFairAll = 67108864;
 
 template <int CH>
 struct TgFmt {
@@ -180,7 +157,7 @@ typedef float f2v __attribute__((ext_vector_type(2)));
 // b = V - m, and the max takes b from the partner through the DPP operand, V' = max(a, dpp(b)).  b is
 // read by DPP 2 slots after its write.  (The three-op form v_add, v_sub_f32_dpp, v_max decides the same;
 // this one is 0.5-1 % faster, profiles/r02/benchab_dpp_forms_8w.log.)
-template <int Q, bool IM = false>
+template <int Q>
 __device__ __forceinline__ void tg_stage_dpp2(float& V, float m)
 {
     float a, b;
@@ -193,8 +170,7 @@ __device__ __forceinline__ void tg_stage_dpp2(float& V, float m)
     else if constexpr (Q == 1) VD_TG_DPP2(MAX, "quad_perm:[2,3,0,1]");                                       \
     else if constexpr (Q == 2) VD_TG_DPP2(MAX, "row_half_mirror");                                           \
     else VD_TG_DPP2(MAX, "row_ror:8");
-    if constexpr (IM) { VD_TG_DPP2Q("v_max_u32_dpp") }
-    else { VD_TG_DPP2Q("v_max_f32_dpp") }
+    VD_TG_DPP2Q("v_max_f32_dpp")
 #undef VD_TG_DPP2Q
 #undef VD_TG_DPP2
 }
@@ -210,18 +186,12 @@ __device__ __forceinline__ float tg_swz16(float V)
 {
     return __builtin_bit_cast(float, __builtin_amdgcn_ds_swizzle(__builtin_bit_cast(int, V), 0x401F));
 }
-__device__ __forceinline__ void tg_stage_lds(float& V, float m, float vp)
-{
-    float t1, t2;
-    asm("v_add_f32 %1, %0, %3\n\tv_sub_f32 %2, %4, %3\n\tv_max_f32 %0, %1, %2"
-        : "+{v60}"(V), "=&v"(t1), "=&v"(t2) : "v"(m), "v"(vp));
-}
-// The same stage with the subtraction before the exchange: b = V - m goes through the LDS crossbar, and
+// The stage with the subtraction before the exchange: b = V - m goes through the LDS crossbar, and
 // since the exchange partners share the label and the tag (every core, except the M_B32 phase-0 stage
 // with its per-half tag sign), the received value is V_partner - m.  After the exchange returns only the
 // max is left, so the round trip's dependent chain is one op shorter; a = V + m issues while it is in
 // flight.
-template <bool X32, bool INT, bool IM = false>
+template <bool X32, bool INT>
 __device__ __forceinline__ void tg_stage_lds_pre(float& V, float m, int paddr)
 {
     float a, b;
@@ -231,51 +201,15 @@ __device__ __forceinline__ void tg_stage_lds_pre(float& V, float m, int paddr)
     if constexpr (INT) asm("v_add_u32 %0, %1, %2" : "=v"(a) : "v"(V), "v"(m));
     else asm("v_add_f32 %0, %1, %2" : "=v"(a) : "v"(V), "v"(m));
     if constexpr (INT) asm("v_max_i32 %0, %1, %2" : "={v60}"(V) : "v"(a), "v"(bp));
-    else if constexpr (IM) asm("v_max_u32 %0, %1, %2" : "={v60}"(V) : "v"(a), "v"(bp));
     else asm("v_max_f32 %0, %1, %2" : "={v60}"(V) : "v"(a), "v"(bp));
 }
 // M_B32 phase-0 stage (S32): V' = max(V + s*m, vp - s*m), s = -1 in the upper position half, where m is
 // the entry of the complementary label (see the kernel)
-template <bool IM = false>
 __device__ __forceinline__ void tg_stage_lds_sg(float& V, float m, float vp, float sg)
 {
     float t1, t2;
-    if constexpr (IM)
-        asm("v_fma_f32 %1, %3, %5, %0\n\tv_fma_f32 %2, -%3, %5, %4\n\tv_max_u32 %0, %1, %2"
-            : "+{v60}"(V), "=&v"(t1), "=&v"(t2) : "v"(m), "v"(vp), "v"(sg));
-    else
-        asm("v_fma_f32 %1, %3, %5, %0\n\tv_fma_f32 %2, -%3, %5, %4\n\tv_max_f32 %0, %1, %2"
-            : "+{v60}"(V), "=&v"(t1), "=&v"(t2) : "v"(m), "v"(vp), "v"(sg));
-}
-
-// The xor-32 / xor-16 stage by a VALU lane swap.  v_permlane32_swap t, u exchanges lanes 32..63 of t with
-// lanes 0..31 of u (v_permlane16_swap: the odd rows of t with the even rows of u).  With the sign s = +1 in
-// the lower member of every exchange pair (lane bit 5 / 4 clear) and -1 in the upper one, t = V + s m and
-// u = V - s m become (own V + m, partner V - m) in every lane after the swap: V' = max(t, u).  The partners
-// share label and tag (every stage but M_B32's phase 0, below).
-template <bool X32>
-__device__ __forceinline__ void tg_stage_perm(float& V, float m, float s)
-{
-    float t, u;
-    if constexpr (X32)
-        asm("v_fma_f32 %1, %3, %4, %0\n\tv_fma_f32 %2, -%3, %4, %0\n\ts_nop 1\n\tv_permlane32_swap_b32 %1, %2\n\t"
-            "v_max_f32 %0, %1, %2"
-            : "+{v60}"(V), "=&v"(t), "=&v"(u) : "v"(s), "v"(m));
-    else
-        asm("v_fma_f32 %1, %3, %4, %0\n\tv_fma_f32 %2, -%3, %4, %0\n\ts_nop 1\n\tv_permlane16_swap_b32 %1, %2\n\t"
-            "v_max_f32 %0, %1, %2"
-            : "+{v60}"(V), "=&v"(t), "=&v"(u) : "v"(s), "v"(m));
-}
-// M_B32 phase 0 (S32) by the lane swap: swapped copies of V put the lower member's metric x in the first
-// and the upper member's y in the second register of every lane; both halves then take max(x + m, y - m)
-// (the lower half's own entry m is E[L]; the upper half's is E[3 - L] and its roles are reversed, see
-// tg_stage_lds_sg)
-__device__ __forceinline__ void tg_stage_perm_sg(float& V, float m)
-{
-    float y, t, u;
-    asm("v_mov_b32 %1, %0\n\ts_nop 1\n\tv_permlane32_swap_b32 %0, %1\n\tv_add_f32 %2, %0, %4\n\t"
-        "v_sub_f32 %3, %1, %4\n\tv_max_f32 %0, %2, %3"
-        : "+{v60}"(V), "=&v"(y), "=&v"(t), "=&v"(u) : "v"(m));
+    asm("v_fma_f32 %1, %3, %5, %0\n\tv_fma_f32 %2, -%3, %5, %4\n\tv_max_f32 %0, %1, %2"
+        : "+{v60}"(V), "=&v"(t1), "=&v"(t2) : "v"(m), "v"(vp), "v"(sg));
 }
 
 // int32 stages (TgFmt::INT): the same forms on integer patterns
@@ -709,7 +643,7 @@ __host__ __device__ __forceinline__ RunGeo seg_run(const SegWG& w, SegPos b0, Se
 __host__ __device__ __forceinline__ int seg_nruns(SegPos b0, SegPos b1) { return b1.i - b0.i + (b1.a != 0 ? 1 : 0); }
 
 // ================================================================ the kernel: one chunk per wave
-template <int CH, int CORE, int OB, int ABL = 0>
+template <int CH, int CORE, int OB>
 __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(8))) void vd_decode_tg(const void* __restrict__ in_all, void* __restrict__ out_all, Geom geo)
 {
     using IN = TgIn<CH>;
@@ -723,7 +657,6 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(8))
     // s = -1 in the upper half (v_fma, as cheap as v_add), and the M_B32 table is the M_B16 one.  SOFT16
     // (INT) keeps the pair rows: each lane reads its own tag sign's half.
     constexpr bool S32 = CORE == B32 && !INT;
-    constexpr bool PRE = !(ABL & kAblPostExchange);  // LDS-exchange stages subtract before the exchange
     // the label-region table (TgTabLT; SOFT16 with its +tag phase-0 area) written with ds_write_addtid_b32
     using TT = TgTabLT<INT>;
     using LL = TgLds<TT::BYTES>;
@@ -770,8 +703,6 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(8))
     const int nrun = seg_nruns(b0, b1);
     // guard words (Geom::check): a uniform branch, nothing when off
     if (geo.check && lane < 3 * kGuardWords) wlds[LL::guard(lane)] = kGuardPattern;
-    const uint64_t t_clk0 = (ABL & kAblClock) ? __builtin_amdgcn_s_memtime() : 0;
-    const uint64_t t_rt0 = (ABL & kAblClock) ? __builtin_amdgcn_s_memrealtime() : 0;
 
     // per-lane LDS byte offset of this position's entry in a phase-K row (row offsets are compile-time)
     const bool upper5 = (pos >> 5) & 1;
@@ -785,7 +716,6 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(8))
     // INT, label regions: the upper half's phase-0 entries come from the +tag area
     if constexpr (INT) aK[0] = upper5 ? TgTabLT<true>::ALT_OFF + 8 * own_label(pos, 0) : aK[0];
     const float sg0 = upper5 ? -1.0f : 1.0f;                  // S32: sign of the phase-0 entry
-    const float sg4 = (pos >> 4) & 1 ? -1.0f : 1.0f;          // kAblX16Perm: upper member of an xor-16 pair
     const int pa5 = 4 * (lane ^ 32);           // ds_bpermute address of the xor-32 partner
     const uint32_t tbk = tb_pack<J, CORE == B32>(lane);  // traceback constants of word kb + lane (kb % 3 == 0)
     // table-build roles: lane l builds the entries at table index l (stage sA) and, lanes 0..31, index
@@ -808,7 +738,7 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(8))
     // In a batched launch only the last batch's waves run the controller: earlier batches' waves are
     // followed by more work on their SIMD, so evening out progress buys nothing there and costs issue
     // (1.6 % per batch, profiles/r02/benchab_fair2.log).
-    if constexpr (!(ABL & kAblNoFair)) fair.begin(batch + 1 < geo.nbatch ? nullptr : geo.fair, lane);
+    fair.begin(batch + 1 < geo.nbatch ? nullptr : geo.fair, lane);
     // fairness progress: blocks started, or in a segment launch the fraction of the segment's pass-0
     // blocks started, scaled to 2^20 (its waves differ in length)
     uint32_t fscale = 1u;
@@ -856,15 +786,14 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(8))
     // ahead; one ds_read_b64 at an even period also carries the entry of the stage 6 later.  The
     // loads are volatile LDS-address-space loads so they stay single ds_read_b64s (2 LDS cycles) in
     // program order -- left alone the compiler merges neighbours into ds_read2_b64 (8 cycles).
-    constexpr int TGD = (ABL & kAblTgd8) ? 8 : 4;  // 6 or 8 measured the same (profiles/r02/ablate_prefetch.log)
+    constexpr int TGD = 4;  // 6 or 8 measured the same (profiles/r02/ablate_prefetch.log)
     typedef __attribute__((address_space(3))) const volatile f2v* lptr;
     const __attribute__((address_space(3))) char* tl = (const __attribute__((address_space(3))) char*)tabb;
     f2v vp[96];  // entry pair read for stage r (the even period of a period pair)
     auto issue = [&](auto Rc) {
         constexpr int r = decltype(Rc)::value;  // stage within the group (the group starts at phase 0)
         constexpr int K = r % 6;
-        if constexpr (ABL & kAblNoTabReads) {
-        } else if constexpr ((r / 6) % 2 == 0) {
+        if constexpr ((r / 6) % 2 == 0) {
             vp[r] = *(lptr)(tl + aK[K] + TT::row(r));
         }
     };
@@ -879,30 +808,23 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(8))
             constexpr int r = 32 * BB + i;  // stage within the group
             constexpr bool ODD = (r / 6) % 2 == 1;
             constexpr int RP = ODD ? r - 6 : r;  // where this stage's pair was read
-            const f2v e = (ABL & kAblNoTabReads) ? (f2v){(float)aK[K], 1.0f} : vp[RP];
+            const f2v e = vp[RP];
             const float m = ODD ? e.y : e.x;
             // Q = 0..3: DPP stage (lane xor 1, 2, 7, 8); Q = 4: xor 16 through ds_swizzle; Q = 5: xor 32
             // through ds_bpermute
             if constexpr (INT) {
                 // (SOFT16's phase-0 entries differ in the tag sign between the xor-32 partners: no pre form)
                 if constexpr (Q <= 3) tg_stage_dpp_i2<Q>(V, m);
-                else if constexpr (Q == 4 && PRE) tg_stage_lds_pre<false, true>(V, m, pa5);
-                else if constexpr (Q == 4) tg_stage_lds_i(V, m, tg_swz16(V));
+                else if constexpr (Q == 4) tg_stage_lds_pre<false, true>(V, m, pa5);
                 else tg_stage_lds_i(V, m, tg_partner(V, pa5));
             } else {
-                constexpr bool IM = (ABL & kAblIntMax) != 0;
-                if constexpr (Q <= 3) tg_stage_dpp2<Q, IM>(V, m);
-                else if constexpr (Q == 4 && (ABL & kAblX16Perm)) tg_stage_perm<false>(V, m, sg4);
-                else if constexpr (Q == 5 && (ABL & kAblX32Perm) && S32) tg_stage_perm_sg(V, m);
-                else if constexpr (Q == 5 && (ABL & kAblX32Perm)) tg_stage_perm<true>(V, m, sg0);
-                else if constexpr (Q == 4 && PRE) tg_stage_lds_pre<false, false, IM>(V, m, pa5);
-                else if constexpr (Q == 4) tg_stage_lds(V, m, tg_swz16(V));
-                else if constexpr (S32) tg_stage_lds_sg<IM>(V, m, tg_partner(V, pa5), sg0);
-                else if constexpr (PRE) tg_stage_lds_pre<true, false, IM>(V, m, pa5);
-                else tg_stage_lds(V, m, tg_partner(V, pa5));
+                if constexpr (Q <= 3) tg_stage_dpp2<Q>(V, m);
+                else if constexpr (Q == 4) tg_stage_lds_pre<false, false>(V, m, pa5);
+                else if constexpr (S32) tg_stage_lds_sg(V, m, tg_partner(V, pa5), sg0);
+                else tg_stage_lds_pre<true, false>(V, m, pa5);
             }
             if constexpr (r + TGD < 96) issue(std::integral_constant<int, r + TGD>{});
-            if constexpr (i % J == J - 1 && !(ABL & kAblNoReadout)) {
+            if constexpr (i % J == J - 1) {
                 // field read-out: bits 1..J of the pattern, (2^(S-1) + h) >> 1 = (h + 2^J - 1) / 2, go straight
                 // into byte / half g of the block's ring word (SDWA dst_sel: one op for shift and merge), then
                 // the field is cleared to 2^(S-1).  At the end of every block (32 stages) the decision-neutral
@@ -942,7 +864,7 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(8))
         if (j >= 2 && (j - 1 - kb == tbn || j == nblk - 1)) {
             wave_sync();
             const uint32_t nw = j - 1 - kb;
-            if (!(ABL & kAblNoTraceback) && (uint32_t)lane < nw && kb + lane >= E) {
+            if ((uint32_t)lane < nw && kb + lane >= E) {
                 const uint32_t k = kb + (uint32_t)lane;
                 // with TBS a multiple of 3 (12: the fp32 cores' label-region table) every batch starts at a
                 // multiple of 3 (batches of TBS - 3 (blockIdx.x & 3) or TBS words), so word k's phase follows
@@ -985,10 +907,6 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(8))
         const float af = (float)A, bf = (float)B;
         const float E0 = __builtin_fmaf(af, -SC, tg0), E1 = __builtin_fmaf(bf, -SC, tg0);
         const float E2 = __builtin_fmaf(bf, SC, tg0), E3 = __builtin_fmaf(af, SC, tg0);
-        if constexpr (ABL & kAblNoTabWrites) {  // tools only: compute the entries, do not store them
-            asm volatile("" ::"v"(E0), "v"(E1), "v"(E2), "v"(E3));
-            return;
-        }
         lds_write_addtid4<256 * part, TgTabL::REGION>(tabl, E0, E1, E2, E3);
     };
     // S01: entries from the two soft values (six FMAs) instead of (A, B) = (s0 + s1, s0 - s1) (two integer
@@ -1008,7 +926,7 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(8))
     for (uint32_t j = j0;; j += 3) {
         // group head: the table from the inputs loaded one group ago, the next group's loads, then the
         // fairness board (its load returns during this group; nothing here waits on it)
-        if constexpr (S01 && !(ABL & kAblNoTabBuild)) {
+        if constexpr (S01) {
             float s0, s1;
             IN::s01(rA, s0, s1);
             put_row_s01(P0{}, s0, s1);
@@ -1016,7 +934,7 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(8))
                 IN::s01(rB, s0, s1);
                 put_row_s01(P1{}, s0, s1);
             }
-        } else if constexpr (!(ABL & kAblNoTabBuild)) {
+        } else {
             using ab_t = std::conditional_t<IN::FAB, float, int>;
             auto ab = [&](const typename IN::raw_t& raw, int l, ab_t& A, ab_t& B) {
                 if constexpr (IN::FAB) IN::abf(raw, l, A, B, geo.scale);
@@ -1030,15 +948,14 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(8))
                 put_row(P1{}, A, B, r6b);
             }
         }
-        if constexpr (!(ABL & kAblNoLoads)) {
+        {  // the next group's input words
             rs = tg_rsrc<CH>(in, start + 32ull * (j + 3), availB);
             rA = IN::template load<0>(rs, vo1);
             rB = IN::template load<0>(rs, vo2);
         }
         // every other group head (6 blocks): 0.7 % faster than every head, every third is 1 % slower
         // (profiles/r02/benchab_fair.log)
-        if constexpr (!(ABL & kAblNoFair))
-            if ((j / 3) % ((ABL & kAblFair4) ? 4 : 2) == 0) fair.group((fdone + j) * fscale, 3u * fscale, lane);
+        if ((j / 3) % 2 == 0) fair.group((fdone + j) * fscale, 3u * fscale, lane);
         if (split && pass == 0 && (int)j == Xspec) vS = V;
         if (split && (int)j == Xcmp) vE = V;
         wave_sync();
@@ -1073,21 +990,12 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(8))
     }
     __syncthreads();  // the next pass overwrites the published vectors read above
     }  // pass
-    if constexpr (!(ABL & kAblNoFair)) fair.end(lane);
+    fair.end(lane);
     if (geo.check) {  // guard words intact?  count the ones that are not
         wave_sync();
         const bool bad = lane < 3 * kGuardWords && wlds[LL::guard(lane)] != kGuardPattern;
         const uint32_t nbad = (uint32_t)__builtin_popcountll(__ballot(bad));
         if (lane == 0 && nbad) atomicAdd(geo.check, nbad);
-    }
-    if constexpr (ABL & kAblClock) {
-        const uint64_t c1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
-        if (lane == 0) {
-            uint64_t* d = (uint64_t*)((char*)out + (16u << 20)) + 6 * (blockIdx.x * kWaves + wv);
-            d[0] = t_clk0; d[1] = c1; d[2] = t_rt0; d[3] = r1;
-            d[4] = (uint32_t)__builtin_amdgcn_s_getreg(4 | (0 << 6) | (31 << 11));
-            d[5] = (uint32_t)__builtin_amdgcn_s_getreg(20 | (0 << 6) | (31 << 11));
-        }
     }
 }
 

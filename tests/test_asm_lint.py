@@ -135,10 +135,10 @@ _TU = """#include "vd_kernel_pk.h"
 template __global__ void vd::vd_decode_pk<vd::HARD, vd::B32>(const void*, void*, vd::Geom);
 template __global__ void vd::vd_decode_pk<vd::FP32, vd::F16>(const void*, void*, vd::Geom);
 template __global__ void vd::vd_decode_pk<vd::SOFT8, vd::B32>(const void*, void*, vd::Geom);
-template __global__ void vd::vd_decode_tg<vd::FP32, vd::F16, 32, 0>(const void*, void*, vd::Geom);
-template __global__ void vd::vd_decode_tg<vd::HARD, vd::B32, 32, 0>(const void*, void*, vd::Geom);
-template __global__ void vd::vd_decode_tg<vd::SOFT8, vd::B16, 32, 0>(const void*, void*, vd::Geom);
-template __global__ void vd::vd_decode_tg<vd::SOFT16, vd::B32, 16, 0>(const void*, void*, vd::Geom);
+template __global__ void vd::vd_decode_tg<vd::FP32, vd::F16, 32>(const void*, void*, vd::Geom);
+template __global__ void vd::vd_decode_tg<vd::HARD, vd::B32, 32>(const void*, void*, vd::Geom);
+template __global__ void vd::vd_decode_tg<vd::SOFT8, vd::B16, 32>(const void*, void*, vd::Geom);
+template __global__ void vd::vd_decode_tg<vd::SOFT16, vd::B32, 16>(const void*, void*, vd::Geom);
 """
 
 

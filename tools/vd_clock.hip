@@ -13,7 +13,7 @@
 #include <random>
 #include <vector>
 #include <algorithm>
-#include "../gpu-accelerated-viterbi-decoder_amd/csrc/vd_kernel_tg.h"
+#include "build/abl/vd_kernel_tg.h"  // the product kernel + tools-only ablation bits (tools/abl/gen_abl.py)
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP error %s at %d\n", hipGetErrorString(e), __LINE__); exit(1); } } while (0)
 using KFn = void (*)(const void*, void*, vd::Geom);
 struct Variant { const char* name; KFn fn; int in; };  // in: 0 HARD, 1 SOFT8, 2 FP32

@@ -72,7 +72,7 @@ int main(int argc, char** argv)
         CK(hipMemcpy(bH + k * strH, hh.data(), hh.size() * 4, hipMemcpyHostToDevice));
         CK(hipMemcpy(bS + k * strS, hs.data(), hs.size() * 4, hipMemcpyHostToDevice));
     }
-    const KFn kh = (KFn)vd::vd_decode_tg<vd::HARD, vd::B32, 32, 0>, ks = (KFn)vd::vd_decode_tg<vd::SOFT8, vd::B16, 32, 0>;
+    const KFn kh = (KFn)vd::vd_decode_tg<vd::HARD, vd::B32, 32>, ks = (KFn)vd::vd_decode_tg<vd::SOFT8, vd::B16, 32>;
     hipEvent_t e0, e1, e2;
     CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1)); CK(hipEventCreate(&e2));
     auto run = [&](int nb, size_t pad, float& th, float& ts) {
@@ -142,7 +142,7 @@ int main(int argc, char** argv)
         char* bF;
         CK(hipMalloc(&bF, strF * steps));
         for (int k = 0; k < steps; k++) CK(hipMemcpy(bF + k * strF, hf.data(), hf.size() * 4, hipMemcpyHostToDevice));
-        const KFn kf = (KFn)vd::vd_decode_tg<vd::FP32, vd::F16, 32, 0>;
+        const KFn kf = (KFn)vd::vd_decode_tg<vd::FP32, vd::F16, 32>;
         std::vector<float> tf[3];
         for (int r = 0; r < rounds; r++)
             for (int v = 0; v < 3; v++) {

@@ -8,7 +8,7 @@
 #include <vector>
 #include <map>
 #include <algorithm>
-#include "../gpu-accelerated-viterbi-decoder_amd/csrc/vd_kernel_tg.h"
+#include "build/abl/vd_kernel_tg.h"  // the product kernel + tools-only ablation bits (tools/abl/gen_abl.py)
 #include "../gpu-accelerated-viterbi-decoder_amd/csrc/vd_segplan.h"
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP error %s at %d\n", hipGetErrorString(e), __LINE__); exit(1); } } while (0)
 using KFn = void (*)(const void*, void*, vd::Geom);
