@@ -189,7 +189,7 @@ __device__ __forceinline__ uint32_t pk8_traceback(uint32_t base, const uint32_t 
         constexpr int BO = EM ? 0 : 2;
         constexpr int c = (BO + 8 * g + 7) % 6;
         constexpr int off = (EM ? 0 : 512) + 256 * (g / 2) + 2 * (g % 2);
-        const uint32_t A = __builtin_amdgcn_bitop3_b32(TX >> sft[c / 2], 0xFCu, base, 0xEA);
+        const uint32_t A = __builtin_amdgcn_bitop3_b32(TX >> (sft[c / 2] & 31u), 0xFCu, base, 0xEA);
         const uint32_t W = *(const __attribute__((address_space(3))) uint8_t*)(uintptr_t)(A + off);
         uint32_t Y = W ^ TX;
         Y = __builtin_amdgcn_bitop3_b32(Y, Y >> 6, 3u, 0x78);  // Y ^ ((Y >> 6) & 3)
@@ -218,7 +218,7 @@ __device__ __forceinline__ uint32_t pk4_traceback(uint32_t base, const uint32_t 
         constexpr int BO = EM ? 0 : 2;
         constexpr int c = (BO + 4 * g + 3) % 6;
         constexpr int off = (EM ? 0 : 512) + g / 2;
-        const uint32_t A = __builtin_amdgcn_bitop3_b32(TX >> sft[c / 2], 0xFCu, base, 0xEA);
+        const uint32_t A = __builtin_amdgcn_bitop3_b32(TX >> (sft[c / 2] & 31u), 0xFCu, base, 0xEA);
         uint32_t W = *(const __attribute__((address_space(3))) uint8_t*)(uintptr_t)(A + off);
         if constexpr (g % 2) W >>= 4;
         const uint32_t T4 = TX >> 4;
@@ -588,7 +588,7 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(SPL
                     // 3 << z; the emit snapshots are rotated right by rho = 2u per 6-bit group (pk2_traceback),
                     // mlo = their low 6 - rho bits: 0x04104104 (2^(6 - rho) - 1)
                     const uint32_t z[3] = {PA, PA >> 8, PA >> 16};
-                    const uint32_t zm[3] = {3u << z[0], 3u << z[1], 3u << z[2]};
+                    const uint32_t zm[3] = {3u << (z[0] & 31u), 3u << (z[1] & 31u), 3u << (z[2] & 31u)};  // (& 31: the shift v_lshlrev does, no C overflow)
                     const uint32_t rho = (PA & 0xFFu) - 2u;
                     const uint32_t mlo = (0x04104104u << (6u - rho)) - 0x04104104u;
                     w = pk2_traceback<CORE>(tbA2, z, zm, rho, mlo);

@@ -14,7 +14,7 @@
 // the winner's history into the lane (a register exchange within the field).  V is kept in [2^23, 2^24)
 // (base 1.25*2^23), where the fp32 ulp is 1 and the low mantissa bits are the low integer bits, and every
 // field starts at 2^(S-1): after J stages the field 2^(S-1) + h is in (0, 2^S), its decision bits
-// (h + 2^J - 1) / 2 are mantissa bits 1..J, and clearing it is one v_and_or_b32.  Renormalising at the end
+// (h + 2^J - 1) / 2 are mantissa bits 1..J, and clearing it is one v_bitop3_b32.  Renormalising at the end
 // of every 32-stage block keeps V in range (bounds below).
 //
 // SOFT16 (|BM| up to 65536: a metric spread near 2^21) leaves no room for the tags below 2^24, so its
@@ -120,18 +120,17 @@ struct TgLds {
     static constexpr int TAB = TABB / 4;                   // table words
     static constexpr int TBS = (kWaveLdsWords - 3 * GW - TAB) / 64 - 1;  // words per traceback batch
     static constexpr int RING = (TBS + 1) * 64;            // ring words
-    static constexpr int TAB_OFF = GW;                     // word offsets within a wave's part
-    static constexpr int RING_OFF = 2 * GW + TAB;
-    static constexpr int WAVE = 3 * GW + TAB + RING;
+    // ring first, its 256-B slots aligned (the OR addressing of tg8_traceback): [ring | guard | table | guard |
+    // guard], a wave's part a multiple of 64 words (word offsets within it)
+    static constexpr int RING_OFF = 0, TAB_OFF = RING + GW;
+    static constexpr int WAVE = (3 * GW + TAB + RING + 63) / 64 * 64;
     // guard word i (0 .. 3 GW - 1) of a wave's part
-    static __device__ __forceinline__ int guard(int i)
-    {
-        return i < GW ? i : i < 2 * GW ? TAB + i : TAB + RING + i;
-    }
+    static __device__ __forceinline__ int guard(int i) { return RING + (i < GW ? i : TAB + i); }
 };
 static_assert(TgLds<TgTabL::BYTES>::TBS == 12 && TgLds<TgTabLT<true>::BYTES>::TBS == 11, "ring lengths");
 static_assert(kWaves * TgLds<TgTabL::BYTES>::WAVE * 4 <= 20480 && kWaves * TgLds<TgTabLT<true>::BYTES>::WAVE * 4 <= 20480,
               "8 workgroups of 4 waves per CU (160 KiB of LDS)");
+static_assert(TgLds<TgTabL::BYTES>::WAVE % 64 == 0 && TgLds<TgTabLT<true>::BYTES>::WAVE % 64 == 0, "ring slots 256-B aligned");
 
 __device__ __forceinline__ int tg_pos(int l)
 {
@@ -348,6 +347,36 @@ __device__ __forceinline__ uint32_t traceback_word_tg(const char* ringb, uint32_
         constexpr int g = G - 1 - decltype(I)::value;
         nat |= field(std::integral_constant<int, 0>{}, std::integral_constant<int, g>{}, slot1 - 256u) << (J * g);
     });
+    return __builtin_bitreverse32(nat);  // word bit i <-> stage 63+32k-i
+}
+// J = 8 (the fp32 cores' SOFT4 / SOFT8 / FP32 and SOFT16's int32 patterns): the same recursion in 2-cycle ops
+// on the ring-first layout (vd_decode_pk's pk8_traceback for one chain).  base = the LDS byte address of the
+// emit slot (256-B aligned; the convergence block is the next slot); sft[c] = TbC::off[c] - 2, so
+// (TX >> sft) & 0xFC is 4 times the position of the state (TX = T * 260: T in bits 2..7 and 8..13); a field:
+// the address by v_lshrrev + v_bitop3 ((t & 0xFC) | base), the byte by ds_read_u8 at a constant offset, Y = W ^
+// TX with the stride-6 fold Y ^= (Y >> 6) & 3, M_B32's raw phase-0 bits back in (v_bitop3 select), the next TX
+// = (Y & 63) * 260, the byte into the word (v_perm) -- where traceback_word_tg's v_bfe / v_lshl_add / v_bfi /
+// v_lshl_or take 4 cycles each
+template <bool FIX5>
+__device__ __forceinline__ uint32_t tg8_traceback(uint32_t base, const uint32_t (&sft)[3], const uint32_t (&m5)[3])
+{
+    uint32_t TX = 0, nat = 0;
+    auto step = [&](auto EMc, auto Gc) {
+        constexpr bool EM = decltype(EMc)::value;
+        constexpr int g = decltype(Gc)::value;
+        constexpr int BO = EM ? 0 : 2;
+        constexpr int c = (BO + 8 * g + 7) % 6;
+        constexpr int off = (EM ? 0 : 256) + g;
+        const uint32_t A = __builtin_amdgcn_bitop3_b32(TX >> (sft[c / 2] & 31u), 0xFCu, base, 0xEA);
+        const uint32_t W = *(const __attribute__((address_space(3))) uint8_t*)(uintptr_t)(A + off);
+        uint32_t Y = W ^ TX;
+        Y = __builtin_amdgcn_bitop3_b32(Y, Y >> 6, 3u, 0x78);  // Y ^ ((Y >> 6) & 3)
+        if constexpr (FIX5) Y = __builtin_amdgcn_bitop3_b32(m5[((BO + 8 * g) % 6) / 2], W, Y, 0xCA);
+        if constexpr (!(EM && g == 0)) TX = __mul24(Y & 63u, 260u);
+        if constexpr (EM) nat = __builtin_amdgcn_perm(Y, nat, (0x03020100u & ~(0xFFu << (8 * g))) | (4u << (8 * g)));
+    };
+    sfor<4>([&](auto I) { step(std::false_type{}, std::integral_constant<int, 3 - decltype(I)::value>{}); });
+    sfor<4>([&](auto I) { step(std::true_type{}, std::integral_constant<int, 3 - decltype(I)::value>{}); });
     return __builtin_bitreverse32(nat);  // word bit i <-> stage 63+32k-i
 }
 
@@ -661,13 +690,14 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(8))
     using TT = TgTabLT<INT>;
     using LL = TgLds<TT::BYTES>;
     constexpr int J = FMT::J, S = FMT::S;
-    __shared__ __attribute__((aligned(16))) uint32_t lds[kWaves * LL::WAVE];
+    __shared__ __attribute__((aligned(256))) uint32_t lds[kWaves * LL::WAVE];
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int pos = tg_pos(lane);
     uint32_t* const wlds = lds + wv * LL::WAVE;
     char* const tabb = (char*)(wlds + LL::TAB_OFF);
     uint32_t* const ring = wlds + LL::RING_OFF;
+    const uint32_t ringl = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)(const char*)ring;  // LDS address
     // This wave's work: chunk blockIdx.x * kWaves + wv, or, in a segment launch (Geom::seg), segment wv of
     // the workgroup's chunks -- see "segment launches" above.
     // A batched launch (Geom::nbatch > 1) decodes chunk c of batch b at launch chunk b * nchunks + c.
@@ -835,7 +865,7 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(8))
                 constexpr int g = (i % 32) / J;
                 uint32_t sr;
 #define VD_TG_RO(SEL, UNUSED) "v_lshrrev_b32_sdwa %[w], 1, %[V] dst_sel:" SEL " dst_unused:" UNUSED             \
-                              " src0_sel:DWORD src1_sel:DWORD\n\tv_and_or_b32 %[V], %[V], %[fnm], %[fhf]"
+                              " src0_sel:DWORD src1_sel:DWORD\n\tv_bitop3_b32 %[V], %[V], %[fnm], %[fhf] bitop3:0xea"
 #define VD_TG_RN "\n\ts_nop 0\n\tv_readfirstlane_b32 %[sr], %[V]\n\ts_sub_u32 %[sr], %[sr], %[vb]\n\tv_subrev_u32 %[V], %[sr], %[V]"
 #define VD_TG_IN [fnm] "v"(fnm), [fhf] "s"(fhf), [vb] "n"(VBASE)  // fhf on the constant bus: one VGPR fewer
                 if constexpr (J == 8 && g == 0)
@@ -871,7 +901,14 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(8))
                 // from the lane; otherwise (SOFT16: 11) from k.  The M_B32 kernels have no VGPR to keep the
                 // lane's constants in (64 at 8 waves per SIMD) and compute them here.
                 const TbC tc = LL::TBS % 3 == 0 && CORE != B32 ? tb_unpack<CORE == B32>(tbk) : tb_direct<J, CORE == B32>((int)k);
-                uint32_t w = traceback_word_tg<J, CORE == B32>((const char*)ring, (uint32_t)(lane + 1) * 256u, tc);
+                uint32_t w;
+                if constexpr (J == 8) {
+                    const uint32_t sft[3] = {tc.off[0] - 2u, tc.off[1] - 2u, tc.off[2] - 2u};
+                    const uint32_t m5[3] = {tc.m50, tc.m50 >> 2, tc.m50 >> 4};  // (traceback_word_tg's m5)
+                    w = tg8_traceback<CORE == B32>(ringl + 256u * (uint32_t)lane, sft, m5);
+                } else {
+                    w = traceback_word_tg<J, CORE == B32>((const char*)ring, (uint32_t)(lane + 1) * 256u, tc);
+                }
                 if constexpr (OB == 32) {
                     ((uint32_t*)out)[wOut + k] = w;
                 } else {
