@@ -8,7 +8,7 @@ or stamps s_memrealtime per wave.  Outputs of ABL != 0 are wrong by design.  Eac
 (product text, tools text) pair that must occur exactly once in the product header: when the product
 kernel changes, the script fails and names the pair to update (tests/test_tools_abl.py runs it on the CPU).
 Tools include "build/abl/vd_kernel_pk.h" (tools/Makefile runs this script first).
-Usage: python3 tools/abl/gen_abl.py [out_dir]
+Usage: python3 tools/abl/gen_abl.py [out_dir] [product csrc dir]
 """
 import os
 import sys
@@ -136,10 +136,10 @@ def apply(text, patches, name, forward=True):
     return text
 
 
-def main(out_dir):
+def main(out_dir, csrc=CSRC):
     os.makedirs(out_dir, exist_ok=True)
     for name, patches in (("vd_kernel_tg.h", TG), ("vd_kernel_pk.h", PK)):
-        src = open(os.path.join(CSRC, name)).read()
+        src = open(os.path.join(csrc, name)).read()
         out = apply(src, patches, name)
         hdr = (f"// GENERATED by tools/abl/gen_abl.py from gpu-accelerated-viterbi-decoder_amd/csrc/{name}: the product\n"
                f"// kernel plus tools-only ablation bits (ABL).  Do not edit; never part of libvitdec.so.\n")
@@ -148,4 +148,6 @@ def main(out_dir):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1] if len(sys.argv) > 1 else os.path.join(ROOT, "tools", "build", "abl"))
+    # [out_dir] [csrc]: another product source tree (A/B of two kernel versions)
+    main(sys.argv[1] if len(sys.argv) > 1 else os.path.join(ROOT, "tools", "build", "abl"),
+         sys.argv[2] if len(sys.argv) > 2 else CSRC)

@@ -16,14 +16,14 @@ import os
 import sys
 from collections import defaultdict
 
-DECODE = {"vd::vd_decode_pk<0, 0, 32, false": "hard_b32", "vd::vd_decode_tg<0, 0, 32,": "hard_b32_tg",
-          "vd::vd_decode_pk<2, 1, 32, false": "soft8_b16", "vd::vd_decode_tg<2, 1, 32,": "soft8_b16_tg",
+DECODE = {"vd::vd_decode_pk<0, 0, 32, false": "hard_b32", "vd::vd_decode_tg<0, 0, 32>": "hard_b32_tg",
+          "vd::vd_decode_pk<2, 1, 32, false": "soft8_b16", "vd::vd_decode_tg<2, 1, 32>": "soft8_b16_tg",
           "vd::vd_decode_pk<10, 1, 32, false": "soft8_b16_llr",
-          "vd::vd_decode_pk<4, 2, 32, false": "fp32_f16", "vd::vd_decode_tg<4, 2, 32,": "fp32_f16_tg",
-          "vd::vd_decode_pk<1, 1, 32, false": "soft4_b16", "vd::vd_decode_tg<1, 1, 32,": "soft4_b16_tg",
-          "vd::vd_decode_tg<3, 0, 32,": "soft16_b32", "vd::vd_decode_pk<0, 0, 16, false": "hard_b32_ob16",
-          "vd::vd_decode_tg<0, 0, 16,": "hard_b32_ob16_tg",
-          "vd::vd_decode_tg<10, 1, 32,": "soft8_b16_llr_tg"}
+          "vd::vd_decode_pk<4, 2, 32, false": "fp32_f16", "vd::vd_decode_tg<4, 2, 32>": "fp32_f16_tg",
+          "vd::vd_decode_pk<1, 1, 32, false": "soft4_b16", "vd::vd_decode_tg<1, 1, 32>": "soft4_b16_tg",
+          "vd::vd_decode_tg<3, 0, 32>": "soft16_b32", "vd::vd_decode_pk<0, 0, 16, false": "hard_b32_ob16",
+          "vd::vd_decode_tg<0, 0, 16>": "hard_b32_ob16_tg",
+          "vd::vd_decode_tg<10, 1, 32>": "soft8_b16_llr_tg"}
 
 
 def short(name):
