@@ -81,7 +81,8 @@ PK = [
      "    uint32_t npass = 0;\n"),
     ("    fair.begin(batch + 1 < geo.nbatch ? nullptr : geo.fair, lane);",
      "    fair.begin(batch + 1 < geo.nbatch && !(ABL & kAblFairAll) ? nullptr : geo.fair, lane);"),
-    ("    uint32_t kb = 0;\n    uint32_t tbn", "    uint32_t kb = 0;\n    uint32_t sink = 0;  // kAblNoStores\n    uint32_t tbn"),
+    ("    uint32_t cpv[kPkChk > 0 ? kPkChk : 1] = {};\n    uint32_t kb = 0;\n",
+     "    uint32_t cpv[kPkChk > 0 ? kPkChk : 1] = {};\n    uint32_t kb = 0;\n    uint32_t sink = 0;  // kAblNoStores\n"),
     ("        if constexpr ((r / 6) % 2 == 0) vp[r] = *(lptr)(tl + aK[K] + TT::row(r));",
      "        if constexpr ((r / 6) % 2 == 0 && !(ABL & kAblNoTabReads)) vp[r] = *(lptr)(tl + aK[K] + TT::row(r));"),
     ("            const uint32_t m = ODD ? vp[RP].y : vp[RP].x;",
