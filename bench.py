@@ -36,7 +36,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md)
 SNR_DB = 2.0
 WARM_S = 0.5      # minimum warm-up (seconds of steps) before the timed region
 POOL = 128        # at most this many resident batches per workload (128 SOFT8 batches: 8.2 GB of input)
-PMC_ROUND = "r05"  # profiles/<round>/: pmc_summary.json, ablate_batched.log, valu_model.json
+PMC_ROUND = "r06"  # profiles/<round>/: pmc_summary.json, ablate_batched.log, valu_model.json
 
 WORKLOADS = [
     ("hard_b32", vitdec.HARD | vitdec.M_B32 | vitdec.O_B32),
