@@ -9,17 +9,19 @@
 //    of every stage pairs positions p and p^(1<<q), q = (t%6+5)%6, and a linear position -> lane map
 //    turns four of the six butterfly distances into DPP controls fused into the ACS max (quad_perm,
 //    row_half_mirror, row_ror:8); xor-16 and xor-32 go through ds_swizzle / ds_bpermute.
-//  * Metric cores.  Every core (M_B32, M_B16, M_FP16) runs in exact-integer fp32, one chunk per wave;
-//    the metric type only selects the tie rule; SOFT16 runs on int32 patterns.
-//  * Survivors.  Tagged ACS (vd_kernel_tg.h): each stage's decision rides in the low bits of the path
-//    metric, so the max itself does the register exchange within an 8- or 16-stage history field; one
-//    SDWA shift per field moves the field's bits into the block's ring word in LDS.  Output words are
-//    traced back lane-parallel, one dependent LDS byte/half read per field, in POSITION space.
+//  * Metric cores.  Two kernels, the same mapping and decisions.  vd_decode_tg (vd_kernel_tg.h): one chunk
+//    per wave, the metric an exact integer in fp32 (SOFT16: int32 patterns); the metric type only selects
+//    the tie rule.  vd_decode_pk (vd_kernel_pk.h): HARD, SOFT4, SOFT8 and FP32 input, two chunks (batched
+//    launches) or two parts of one chunk (split single launches) per wave, one in each exact-integer
+//    16-bit half of the metric word (v_add_u32, v_sub_u32_dpp, v_pk_max_u16 per stage for both).
+//  * Survivors.  Tagged ACS: each stage's decision rides in the low bits of the path metric, so the max
+//    itself does the register exchange within a history field (16, 8, 4 or 2 stages by format); the
+//    fields' bits go into the block's survivor ring in LDS.  Output words are traced back lane-parallel,
+//    one dependent LDS read per field, in POSITION space.
 //  * Branch metrics.  Per 96-stage group, every lane builds table rows (the four label entries of one
 //    stage) into LDS; every stage each lane reads its own transition's entry (one ds_read_b64 serves
 //    two stages of the same phase).
-// This file holds the shared pieces (geometry, chunk partition, fairness controller); vd_kernel_tg.h
-// holds the decode kernel.
+// This file holds the shared pieces (geometry, chunk partition, fairness controller).
 //
 // Decode semantics (bit-exact with the reference for every valid option): see DESIGN.md and
 // oracle/vd_oracle.c.  Tie rules, in own/exchanged terms: M_B16 -> exchanged wins, M_FP16 -> own
