@@ -1,16 +1,17 @@
-// dataflow.h -- minimal linear element pipeline for the simulation harness.
-// Interface-compatible with the reference's src/dataflow/dataflow.h (ComputeElement, Pipeline,
-// PipelineResult, operator|, probe(), per-element status with "Elapsed run time"), so the CLI and
-// viterbiDF.h read the same; host-only, no GPU knowledge.
+// dataflow.h -- the simulation harness's linear element chain (host only, no GPU knowledge).
+// The CLI (main.cpp) and the harness elements (viterbiDF.h) are written against the reference's
+// src/dataflow/dataflow.h interface, so this keeps its names and printed report: ComputeElement with
+// process() / probe() / a per-element status map, Pipeline built with operator|, run() returning the
+// final output plus the outputs of probed elements, printStatus() with each element's "Elapsed run time".
 #pragma once
 
 #include <any>
 #include <chrono>
-#include <iomanip>
+#include <cstdio>
+#include <functional>
 #include <iostream>
 #include <map>
 #include <optional>
-#include <sstream>
 #include <stdexcept>
 #include <string>
 #include <typeinfo>
@@ -18,37 +19,49 @@
 
 using OptData = std::optional<std::any>;
 
+namespace dataflow_detail {
+// "12.34 s" / "56.78 ms" / "910 us", as the reference's report prints an element's run time
+inline std::string elapsed_text(std::chrono::microseconds d)
+{
+    const long long us = d.count();
+    char buf[64];
+    if (us > 1000000) std::snprintf(buf, sizeof buf, "%.2f s", us * 1e-6);
+    else if (us > 1000) std::snprintf(buf, sizeof buf, "%.2f ms", us * 1e-3);
+    else std::snprintf(buf, sizeof buf, "%lld us", us);
+    return buf;
+}
+constexpr const char* kElapsed = "Elapsed run time";
+}  // namespace dataflow_detail
+
+// One element of the chain: a source when its input is empty (std::nullopt), else a transform.
 class ComputeElement {
+    std::map<std::string, std::any> entries_;
+    bool tapped_ = false;
+
 public:
     virtual ~ComputeElement() = default;
-    // in == std::nullopt for a source element
     virtual std::any process(const OptData& in) = 0;
 
-    ComputeElement& probe() { probed_ = true; return *this; }
-    bool isProbed() const { return probed_; }
+    // mark the element so that Pipeline::run keeps a copy of its output
+    ComputeElement& probe()
+    {
+        tapped_ = true;
+        return *this;
+    }
+    bool isProbed() const { return tapped_; }
 
-    void setStatus(const std::string& key, std::any v) { status_[key] = std::move(v); }
-    std::any getStatus(const std::string& key) const { return status_.at(key); }
-    const std::map<std::string, std::any>& getStatusMap() const { return status_; }
+    void setStatus(const std::string& key, std::any v) { entries_[key] = std::move(v); }
+    std::any getStatus(const std::string& key) const { return entries_.at(key); }
+    const std::map<std::string, std::any>& getStatusMap() const { return entries_; }
 
+    // elements override this for the status entries they know how to print
     virtual std::string getStatusString(const std::string&) const { return "(Not printable)"; }
     std::string getStatusStringAll(const std::string& key) const
     {
-        if (key != "Elapsed run time") return getStatusString(key);
-        const double us = (double)std::any_cast<std::chrono::microseconds>(status_.at(key)).count();
-        std::ostringstream os;
-        os << std::fixed << std::setprecision(2);
-        if (us > 1e6) os << us / 1e6 << " s";
-        else if (us > 1e3) os << us / 1e3 << " ms";
-        else os << std::setprecision(0) << us << " us";
-        return os.str();
+        if (key == dataflow_detail::kElapsed)
+            return dataflow_detail::elapsed_text(std::any_cast<std::chrono::microseconds>(entries_.at(key)));
+        return getStatusString(key);
     }
-
-protected:
-    std::map<std::string, std::any> status_;
-
-private:
-    bool probed_ = false;
 };
 
 struct PipelineResult {
@@ -57,40 +70,54 @@ struct PipelineResult {
 };
 
 class Pipeline {
-public:
-    Pipeline& add(ComputeElement& e) { stages_.push_back(&e); return *this; }
+    std::vector<std::reference_wrapper<ComputeElement>> chain_;
 
+public:
+    Pipeline& add(ComputeElement& e)
+    {
+        chain_.emplace_back(e);
+        return *this;
+    }
+
+    // each element's output feeds the next; every element's wall time goes into its status map
     PipelineResult run()
     {
-        PipelineResult r;
-        OptData cur;
-        for (ComputeElement* e : stages_) {
-            const auto t0 = std::chrono::high_resolution_clock::now();
-            cur = e->process(cur);
-            const auto t1 = std::chrono::high_resolution_clock::now();
-            e->setStatus("Elapsed run time", std::chrono::duration_cast<std::chrono::microseconds>(t1 - t0));
-            if (e->isProbed()) r.probed_outputs.push_back(*cur);
+        PipelineResult out;
+        OptData data;
+        for (ComputeElement& e : chain_) {
+            const auto begin = std::chrono::high_resolution_clock::now();
+            data = e.process(data);
+            e.setStatus(dataflow_detail::kElapsed, std::chrono::duration_cast<std::chrono::microseconds>(
+                                                       std::chrono::high_resolution_clock::now() - begin));
+            if (e.isProbed()) out.probed_outputs.push_back(*data);
         }
-        if (!cur) throw std::runtime_error("Pipeline produced no output");
-        r.final_output = std::move(*cur);
-        return r;
+        if (!data.has_value()) throw std::runtime_error("Pipeline produced no output");
+        out.final_output = std::move(*data);
+        return out;
     }
 
     void printStatus() const
     {
         std::cout << "--- Pipeline Status ---\n";
-        for (size_t i = 0; i < stages_.size(); i++) {
-            std::cout << "Element " << i << " (type: " << typeid(*stages_[i]).name() << "):\n";
-            const auto& m = stages_[i]->getStatusMap();
-            if (m.empty()) std::cout << "  - No status information.\n";
-            for (const auto& kv : m) std::cout << "  - " << kv.first << ": " << stages_[i]->getStatusStringAll(kv.first) << "\n";
+        size_t idx = 0;
+        for (const ComputeElement& e : chain_) {
+            std::cout << "Element " << idx++ << " (type: " << typeid(e).name() << "):\n";
+            if (e.getStatusMap().empty()) std::cout << "  - No status information.\n";
+            for (const auto& entry : e.getStatusMap())
+                std::cout << "  - " << entry.first << ": " << e.getStatusStringAll(entry.first) << "\n";
         }
         std::cout << "--- End of Status ---\n";
     }
-
-private:
-    std::vector<ComputeElement*> stages_;
 };
 
-inline Pipeline operator|(ComputeElement& a, ComputeElement& b) { Pipeline p; p.add(a).add(b); return p; }
-inline Pipeline operator|(Pipeline p, ComputeElement& b) { p.add(b); return p; }
+inline Pipeline operator|(ComputeElement& first, ComputeElement& second)
+{
+    Pipeline p;
+    p.add(first).add(second);
+    return p;
+}
+inline Pipeline operator|(Pipeline p, ComputeElement& next)
+{
+    p.add(next);
+    return p;
+}

@@ -8,8 +8,10 @@
 
 #include <cmath>
 #include <cstdint>
+#include <iomanip>
 #include <limits>
 #include <random>
+#include <sstream>
 #include <vector>
 
 #include "dataflow.h"
