@@ -166,6 +166,39 @@ def trace_word_kernel(ring, k):
     return int("{:032b}".format(nat)[::-1], 2)  # bitreverse: word bit i <-> stage 63 + 32k - i
 
 
+def trace_word_skewed(ring, k, tbl):
+    """trace_word_kernel on a skewed ring (round 6 study, not in the product: exact, 19 % fewer SOFT8 bank
+    conflicts, 1.5 % slower; profiles/r06/ab_ring_skew/): slot s keeps position p' at dword p' ^ s; lane tbl's
+    emit slot is tbl, its convergence slot tbl + 1.  A starts at 4 (tbl + 1), xt re-skews it between the
+    blocks, cn takes the emit skew out of the snapshots (and out of field 0's pair)."""
+    u = (k + 2) % 3
+    z = [2 * ((u + r) % 3) + 2 for r in range(3)]
+    xt = 4 * ((tbl + 1) ^ tbl)
+    cn = (4 * tbl * 0x01041041) & 0xFFFFFFFF
+    A = 4 * (tbl + 1)
+    nat = 0
+    for blk, EM, s in ((k + 2, False, tbl + 1), (k + 1, True, tbl)):
+        stored = [ring[16 * blk + g] for g in range(16)]
+        for g in range(15, -1, -1):
+            row = [stored[g][q ^ s] for q in range(64)]  # the writer's dword p' ^ s holds position p'
+            d = row[A >> 2]
+            zz = z[(g + 2) % 3] if EM else z[g % 3]
+            A ^= d << zz
+            if EM and g % 3 == 1:
+                nat |= ((A >> 2) & 63) << (2 * g)
+            if EM and g == 0:
+                nat |= ((A ^ (cn & 0xFC)) >> zz) & 3
+        if not EM:
+            A ^= xt
+    nat ^= cn
+    rho = 2 * u
+    mlo = {0: 0xFFFFFFFC, 2: 0x3CF3CF3C, 4: 0x0C30C30C}[rho]
+    grp = nat & ~3 & 0xFFFFFFFF
+    a, b = grp >> rho, (grp << (6 - rho)) & 0xFFFFFFFF
+    nat = (nat & 3) | (a & mlo) | (b & ~mlo & 0xFFFFFFFF)
+    return int("{:032b}".format(nat)[::-1], 2)
+
+
 def run(AB, core):
     dec = ref_acs(AB, core)
     ring, lo, hi, spread = model(AB, core)
@@ -177,9 +210,11 @@ def run(AB, core):
         a = trace_word(ring, k)
         b = ref_traceback(dec, 32 * k + 95, 64)
         w = trace_word_kernel(ring, k)
+        ws = trace_word_skewed(ring, k, k % 7)
         for t in range(32 * k + 32, 32 * k + 64):
             bad += a[t] != b[t]
             bad += ((w >> (63 + 32 * k - t)) & 1) != b[t]
+            bad += ((ws >> (63 + 32 * k - t)) & 1) != b[t]
     return bad, lo, hi, spread
 
 
